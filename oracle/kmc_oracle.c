@@ -1,0 +1,169 @@
+/*
+ * kmc_oracle.c — TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * Plain-C restatement of the reference's k-mer counting path
+ * (axlwild/dna-kmeres-parallel).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library; the product path
+ * (dna-kmeres-parallel_amd/) never links or calls it.
+ *
+ * Parity pinning: this restatement is checked in tests/test_oracle.py against
+ *   (1) golden vectors in tests/golden/ produced by oracle/_ref, which compiles the
+ *       reference's OWN permutationsCountAll (main.cu:636-646) and permutation()
+ *       (utils.h:21-50) from /root/reference (recipe: oracle/Makefile), and
+ *   (2) the live oracle/_ref library when it is present.
+ *
+ * Semantics restated:
+ *   - record s occupies data[indices[s] .. indices[s+1]) including one terminator
+ *     byte; entryLength E = indices[s+1]-indices[s]            (kernels.h:124)
+ *   - windows start at offsets i = 0 .. E-k-1                  (kernels.h:133, main.cu:641)
+ *   - bin order is little-endian in the window position: the code of a window is
+ *     sum_p code(x[i+p]) * 4^p with A=0,C=1,G=2,T=3            (utils.h:35-47)
+ *   - a window holding any byte outside {A,C,G,T} is counted in the CPU path's
+ *     bin 0 (main.cu:643-644) and dropped by the GPU path (kernels.h:136-139)
+ *   - GPU output layout: sum[s + num_seqs*code], int32, overwritten (kernels.h:142)
+ *   - CPU output layout: countResults[1 + code], countResults[0] = invalid (main.cu:598-603)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* A=0 C=1 G=2 T=3, everything else -1 (uppercase only, as permutationsMap keys are). */
+static int base_code(unsigned char c) {
+    switch (c) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        default: return -1;
+    }
+}
+
+/* Number of windows of a record of entry length E (terminator included). */
+static int64_t n_windows(int64_t E, int k) {
+    int64_t n = E - (int64_t)k;
+    return n > 0 ? n : 0;
+}
+
+/*
+ * Histogram of one record in the CPU layout of permutationsCountAll
+ * (main.cu:636-646): hist[0] = invalid windows, hist[1 + code] = count.
+ * `rec` points at the record's first byte, E = entry length incl. terminator.
+ * hist must hold 4^k + 1 ints (k <= 15).
+ */
+void oracle_count_record_cpu(const char *rec, int64_t E, int k, int32_t *hist) {
+    const uint64_t nbins = (uint64_t)1 << (2 * k);
+    memset(hist, 0, (nbins + 1) * sizeof(int32_t));
+    const int64_t nw = n_windows(E, k);
+    if (nw == 0) return;
+    /* rolling LE code: code = (code >> 2) | (b << 2(k-1)); run = valid bases ending here */
+    uint64_t code = 0;
+    int run = 0;
+    const int shift = 2 * (k - 1);
+    /* prime with the first k-1 bases */
+    for (int64_t i = 0; i < nw + k - 1; ++i) {
+        int b = base_code((unsigned char)rec[i]);
+        if (b < 0) {
+            run = 0;
+            code = 0;
+        } else {
+            code = (code >> 2) | ((uint64_t)b << shift);
+            ++run;
+        }
+        int64_t start = i - (k - 1);
+        if (start < 0) continue;
+        if (run >= k)
+            hist[1 + code]++;
+        else
+            hist[0]++;
+    }
+}
+
+/*
+ * GPU-layout dense histogram over all records (the contract of
+ * sumKmereCoincidencesGlobalMemory, generalised to any k as the CPU path is):
+ * sum[s + ld*code] for code < 4^k; invalid[s] (optional) = CPU bin 0.
+ */
+void oracle_count_dense(const char *data, const int64_t *indices, int64_t num_seqs, int k,
+                        int32_t *sum, int64_t ld, int32_t *invalid) {
+    const uint64_t nbins = (uint64_t)1 << (2 * k);
+    if (ld == 0) ld = num_seqs;
+    int32_t *hist = (int32_t *)malloc((nbins + 1) * sizeof(int32_t));
+    for (int64_t s = 0; s < num_seqs; ++s) {
+        const int64_t E = indices[s + 1] - indices[s];
+        oracle_count_record_cpu(data + indices[s], E, k, hist);
+        for (uint64_t c = 0; c < nbins; ++c) sum[s + ld * (int64_t)c] = hist[1 + c];
+        if (invalid) invalid[s] = hist[0];
+    }
+    free(hist);
+}
+
+/*
+ * Windowed variant used to check byte-range sharding: only windows whose start
+ * position p (absolute offset into data) lies in [win_lo, win_hi) are counted.
+ */
+void oracle_count_dense_range(const char *data, const int64_t *indices, int64_t num_seqs, int k,
+                              int64_t win_lo, int64_t win_hi, int32_t *sum, int64_t ld,
+                              int32_t *invalid) {
+    const uint64_t nbins = (uint64_t)1 << (2 * k);
+    const uint64_t mask = nbins - 1;
+    if (ld == 0) ld = num_seqs;
+    for (int64_t s = 0; s < num_seqs; ++s) {
+        for (uint64_t c = 0; c < nbins; ++c) sum[s + ld * (int64_t)c] = 0;
+        if (invalid) invalid[s] = 0;
+        const int64_t a = indices[s];
+        const int64_t nw = n_windows(indices[s + 1] - a, k);
+        for (int64_t i = 0; i < nw; ++i) {
+            const int64_t p = a + i;
+            if (p < win_lo || p >= win_hi) continue;
+            uint64_t code = 0;
+            int ok = 1;
+            for (int q = 0; q < k; ++q) {
+                int b = base_code((unsigned char)data[p + q]);
+                if (b < 0) { ok = 0; break; }
+                code |= (uint64_t)b << (2 * q);
+            }
+            if (ok)
+                sum[s + ld * (int64_t)(code & mask)]++;
+            else if (invalid)
+                invalid[s]++;
+        }
+    }
+}
+
+/* LE code of one window (helper for tests); returns -1 when invalid. */
+int64_t oracle_window_code(const char *w, int k) {
+    uint64_t code = 0;
+    for (int q = 0; q < k; ++q) {
+        int b = base_code((unsigned char)w[q]);
+        if (b < 0) return -1;
+        code |= (uint64_t)b << (2 * q);
+    }
+    return (int64_t)code;
+}
+
+/*
+ * Pairwise k-mer distance of the reference's step 2 (main.cu:604-619, kernels.h:85-109):
+ * d(i,j) = 1 - sum_p min(c_i[p], c_j[p]) / (min(L_i, L_j) - k + 1), packed strict upper
+ * triangle, row-major, index getIdxTriangularMatrixRowMajorSeq(i+1, j-i, n) (main.cu:671-673).
+ * counts: GPU layout sum[s + n*code]; lens[s] = L_s = entry length - 1.
+ * The division is done in float as in the reference ((float)sum / long -> float).
+ */
+static long tri_idx(long i, long j, long n) {
+    return (n * (i - 1) - (((i - 2) * (i - 1)) / 2)) + (j - i);
+}
+
+void oracle_pair_distances(const int32_t *sum, const int64_t *lens, int64_t n, int k, float *out) {
+    const uint64_t nbins = (uint64_t)1 << (2 * k);
+    for (long i = 0; i < n - 1; ++i) {
+        for (long j = i + 1; j < n; ++j) {
+            long minLength = lens[i] < lens[j] ? (long)lens[i] : (long)lens[j];
+            long acc = 0;
+            for (uint64_t p = 0; p < nbins; ++p) {
+                int32_t a = sum[i + n * (int64_t)p], b = sum[j + n * (int64_t)p];
+                acc += a < b ? a : b;
+            }
+            float d = 1 - (float)acc / (minLength - k + 1);
+            out[tri_idx(i + 1, j - i, n)] = d;
+        }
+    }
+}
