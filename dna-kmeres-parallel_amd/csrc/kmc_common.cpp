@@ -1,0 +1,21 @@
+// kmc_common.cpp — error strings and version of libkmc.so.
+#include <hip/hip_runtime.h>
+
+#include "kmc.h"
+
+extern "C" const char *kmc_error_string(int code) {
+    switch (code) {
+        case KMC_OK: return "success";
+        case KMC_ERR_INVALID_ARG: return "invalid argument";
+        case KMC_ERR_UNSUPPORTED_K: return "k outside the supported range of this entry point";
+        case KMC_ERR_ALIGNMENT: return "data pointer must be 16-byte aligned";
+        case KMC_ERR_WORKSPACE: return "workspace smaller than the required size";
+        case KMC_ERR_IO: return "file cannot be opened or read";
+        case KMC_ERR_NOMEM: return "allocation failed";
+        case KMC_ERR_RCCL: return "RCCL call failed";
+        case KMC_ERR_NO_DEVICE: return "no HIP device visible";
+        default: return hipGetErrorString(static_cast<hipError_t>(code));
+    }
+}
+
+extern "C" int kmc_version(void) { return 100; }  // 0.1.0

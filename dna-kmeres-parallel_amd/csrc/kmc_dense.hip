@@ -1,0 +1,811 @@
+// kmc_dense.hip — dense k-mer histogram kernels for gfx950 (MI355X, CDNA4).
+//
+// Replaces sumKmereCoincidencesGlobalMemory (reference kernels.h:113-144), which
+// gives one block per record and one thread per pattern, every thread rescanning
+// its record with 3-byte compares.  Here one pass reads every byte once:
+//
+//   HBM --dwordx4--> lane registers: 16 ASCII bases per lane per tile (1 KiB/wave)
+//       --SWAR-----> 32-bit 2-bit-packed codes (first base in the low bits, i.e.
+//                    the reference's little-endian bin order) + 16-bit invalid mask
+//       --shfl-----> the next lane's codes as the (k-1)-base halo
+//       --bfe------> 16 window codes per lane, one LDS atomic each
+//       --flush----> per-record histogram, written once (direct or via slab reduce)
+//
+// Layout of the work: the buffer is cut into 1 KiB tiles; workgroup w owns a
+// contiguous tile range and walks the records intersecting it ("pieces").  A
+// piece covering a whole record is written straight to sum[]; the (at most two)
+// partial pieces of a workgroup go to a slab, summed per record by
+// reduce_dense_kernel.  No global atomics on the hot path.
+//
+// Histogram storage per workgroup (LDS):
+//   k <= 7 : 32-bit counters, R replicas interleaved (bin*R + lane%R) so lanes of a
+//            32-lane LDS group never collide on small alphabets (k <= 4: R = 32).
+//   k == 8 : 65 536 bins do not fit as 32-bit (256 KB > 160 KB LDS): two 16-bit
+//            counters per word (bin c in the low half, c|0x8000 in the high
+//            half).  ds_add_rtn reports the rare half-wrap; the lost 65 536 are
+//            recorded as a spill entry and re-added by spill_apply_kernel.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+#include <vector>
+
+#include "kmc.h"
+#include "kmc_internal.h"
+
+namespace kmc {
+namespace {
+
+constexpr int kTileShift = 10;  // 1 KiB per wave per tile
+constexpr int kTile = 1 << kTileShift;
+
+struct Spill {
+    int64_t rec;
+    int32_t code;
+    int32_t amount;
+};
+
+struct Params {
+    const char *data;
+    const void *indices;
+    int64_t n;
+    int32_t *sum;
+    int64_t ld;
+    int32_t *invalid;
+    int64_t wl, wh, rl, rh;  // window range, readable range (derive == 0)
+    int derive;              // 1: both ranges = [indices[0], indices[n])
+    int G;                   // workgroups of the count kernel
+    uint32_t *slab;          // [G][2][4^k]
+    int64_t *slot_rec;       // [G][2] record held by each slab slot, -1 = none
+    Spill *spill;            // [G][spill_cap]
+    uint32_t *spill_cnt;     // [G]
+    uint32_t spill_cap;
+};
+
+struct Geom {
+    int64_t wl, wh, rl, rh;
+    int64_t T0, T1, tpw;
+};
+
+template <class Idx>
+__device__ __forceinline__ int64_t rec_off(const Params &p, int64_t i) {
+    return (int64_t)((const Idx *)p.indices)[i];
+}
+
+template <class Idx>
+__device__ __forceinline__ Geom make_geom(const Params &p) {
+    Geom g;
+    if (p.derive) {
+        g.wl = rec_off<Idx>(p, 0);
+        g.wh = rec_off<Idx>(p, p.n);
+        g.rl = g.wl;
+        g.rh = g.wh;
+    } else {
+        g.wl = p.wl;
+        g.wh = p.wh;
+        g.rl = p.rl;
+        g.rh = p.rh;
+    }
+    if (g.wh <= g.wl) {
+        g.T0 = g.T1 = 0;
+        g.tpw = 1;
+    } else {
+        g.T0 = g.wl >> kTileShift;
+        g.T1 = (g.wh + kTile - 1) >> kTileShift;
+        g.tpw = (g.T1 - g.T0 + p.G - 1) / p.G;
+    }
+    return g;
+}
+
+// Window range of record s clipped to the counted range: [ca, ce).
+template <int K, class Idx>
+__device__ __forceinline__ void record_windows(const Params &p, const Geom &g, int64_t s, int64_t &ca,
+                                               int64_t &ce) {
+    const int64_t a = rec_off<Idx>(p, s);
+    const int64_t e = rec_off<Idx>(p, s + 1);
+    const int64_t nw = e - a - K > 0 ? e - a - K : 0;  // kernels.h:133 generalised
+    ca = a > g.wl ? a : g.wl;
+    ce = (a + nw) < g.wh ? (a + nw) : g.wh;
+}
+
+// 16 ASCII bytes -> 2-bit LE codes (A0 C1 G2 T3) and a 1-bit-per-base invalid mask.
+//   code(b) = ((b >> 1) ^ (b >> 2)) & 3 maps A,C,G,T to 0,1,2,3; a byte is valid iff
+//   it equals the canonical letter of its code (v_perm_b32 as a 4-entry table).
+__device__ __forceinline__ void pack16(const uint4 r, uint32_t &code, uint32_t &bad) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    code = 0;
+    bad = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t c = ((w[d] >> 1) ^ (w[d] >> 2)) & 0x03030303u;
+        const uint32_t canon = __builtin_amdgcn_perm(0u, 0x54474341u, c);  // "ACGT"[c] per byte
+        const uint32_t x = w[d] ^ canon;
+        const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        const uint32_t b4 = (((nz >> 7) * 0x00204081u) >> 21) & 0xFu;
+        const uint32_t q = c | (c >> 6);
+        const uint32_t p8 = (q & 0xFu) | ((q >> 12) & 0xF0u);
+        code |= p8 << (8 * d);
+        bad |= b4 << (4 * d);
+    }
+}
+
+__device__ __forceinline__ uint4 load_chunk(const char *data, int64_t q, int64_t rl, int64_t rh) {
+    if (q >= rl && q + 16 <= rh) return *reinterpret_cast<const uint4 *>(data + q);
+    uint32_t v[4] = {0u, 0u, 0u, 0u};
+    for (int i = 0; i < 16; ++i) {
+        const int64_t b = q + i;
+        if (b >= rl && b < rh) v[i >> 2] |= (uint32_t)(uint8_t)data[b] << (8 * (i & 3));
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// OR of x >> 0 .. x >> (K-1): bit j set iff any of bases j .. j+K-1 is invalid.
+template <int K>
+__device__ __forceinline__ uint32_t smear(uint32_t x) {
+    uint32_t s = x;
+    int c = 1;
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+        if (c < K) {
+            const int st = (c < K - c) ? c : (K - c);
+            s |= s >> st;
+            c += st;
+        }
+    }
+    return s;
+}
+
+// Per-piece context of the k == 8 packed-16-bit histogram.
+struct P16Ctx {
+    uint32_t *h;
+    uint32_t *spill_n;  // LDS counter
+    Spill *spill;       // this workgroup's slice
+    uint32_t cap;
+    int64_t rec;
+};
+
+__device__ __forceinline__ void p16_spill(const P16Ctx &c, int32_t code, int32_t amount) {
+    const uint32_t i = atomicAdd(c.spill_n, 1u);
+    if (i < c.cap) {
+        Spill e;
+        e.rec = c.rec;
+        e.code = code;
+        e.amount = amount;
+        c.spill[i] = e;
+    }
+}
+
+// A half of a packed word wrapped (the returned old value had 0xFFFF in the half
+// that was incremented): record the exact correction, and undo a carry from the
+// low half into the high half.  Every wrap of either 16-bit field is observed
+// exactly once, by the atomic that caused it (forward: the add that saw 0xFFFF;
+// backward: the carry removal that saw 0), so the spill entries plus the final
+// field values reconstruct the true counts for any interleaving of the waves.
+//   hb      1 if the window incremented the high half
+//   hiwrap  the low-half add also found the high half at 0xFFFF (carry wrapped it)
+__device__ __noinline__ void p16_fix(const P16Ctx &c, uint32_t word, uint32_t hb, uint32_t hiwrap) {
+    if (hb == 0u) {
+        p16_spill(c, (int32_t)word, 65536);
+        if (hiwrap) p16_spill(c, (int32_t)(word | 0x8000u), 65536);
+        const uint32_t o2 = __hip_atomic_fetch_add(&c.h[word], 0xFFFF0000u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((o2 >> 16) == 0u) p16_spill(c, (int32_t)(word | 0x8000u), -65536);
+    } else {
+        p16_spill(c, (int32_t)(word | 0x8000u), 65536);
+    }
+}
+
+// Count the windows of one tile for one lane.  lo = codes of the lane's 16 bases,
+// hi = codes of the next 16 (halo), W = 16-bit mask of windows to count.
+template <int K, int R, bool P16>
+__device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W, bool full, uint32_t *h,
+                                           int lane, const P16Ctx &pc) {
+    const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);  // bases 8..23
+    if constexpr (!P16) {
+        const uint32_t rep = (uint32_t)(lane & (R - 1));
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint32_t code;
+                if (j <= 16 - K) code = (lo >> (2 * j)) & ((1u << (2 * K)) - 1u);
+                else code = (mid >> (2 * (j - 8))) & ((1u << (2 * K)) - 1u);
+                __hip_atomic_fetch_add(&h[code * R + rep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint32_t code;
+                if (j <= 16 - K) code = (lo >> (2 * j)) & ((1u << (2 * K)) - 1u);
+                else code = (mid >> (2 * (j - 8))) & ((1u << (2 * K)) - 1u);
+                if ((W >> j) & 1u)
+                    __hip_atomic_fetch_add(&h[code * R + rep], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    } else {
+        static_assert(K == 8, "packed 16-bit histogram is the k == 8 layout");
+        uint32_t old[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t src = (j <= 8) ? lo : mid;
+            const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
+            const uint32_t word = (src >> off) & 0x7FFFu;
+            const uint32_t hb = (src >> (off + 15)) & 1u;
+            const uint32_t inc = hb ? 0x10000u : 1u;
+            old[j] = 0u;
+            if (full || ((W >> j) & 1u))
+                old[j] = __hip_atomic_fetch_add(&h[word], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // checks after all 16 adds are in flight (LDS returns in order: counted waits)
+        uint32_t ovf = 0u, hw = 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t src = (j <= 8) ? lo : mid;
+            const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
+            const uint32_t hb = (src >> (off + 15)) & 1u;
+            const uint32_t m = hb ? 0xFFFF0000u : 0x0000FFFFu;
+            ovf |= (uint32_t)((old[j] & m) == m) << j;
+            hw |= (uint32_t)(old[j] >= 0xFFFF0000u) << j;
+        }
+        if (!full) ovf &= W;
+        if (__any(ovf != 0u)) {
+            const uint64_t both = (uint64_t)lo | ((uint64_t)hi << 32);
+            for (int j = 0; j < 16; ++j) {
+                if ((ovf >> j) & 1u) {
+                    const uint32_t code = (uint32_t)(both >> (2 * j)) & 0xFFFFu;
+                    p16_fix(pc, code & 0x7FFFu, code >> 15, (hw >> j) & 1u);
+                }
+            }
+        }
+    }
+}
+
+// One wave counts the windows of tiles [t0, t1) that start in [ps, pe).
+template <int K, int R, bool P16>
+__device__ void count_wave_range(const char *data, int64_t t0, int64_t t1, int64_t ps, int64_t pe, int64_t rl,
+                                 int64_t rh, uint32_t *h, int lane, const P16Ctx &pc) {
+    if (t0 >= t1) return;
+    const int64_t lane_off = (int64_t)lane * 16;
+    uint4 r_nxt = load_chunk(data, ((t0 + 1) << kTileShift) + lane_off, rl, rh);
+    uint32_t c_cur, b_cur;
+    pack16(load_chunk(data, (t0 << kTileShift) + lane_off, rl, rh), c_cur, b_cur);
+    for (int64_t t = t0; t < t1; ++t) {
+        uint4 r_nn = make_uint4(0u, 0u, 0u, 0u);
+        if (t + 2 <= t1) r_nn = load_chunk(data, ((t + 2) << kTileShift) + lane_off, rl, rh);
+        uint32_t c_nxt, b_nxt;
+        pack16(r_nxt, c_nxt, b_nxt);
+        // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
+        uint32_t hc = __shfl_down(c_cur, 1);
+        uint32_t hbad = __shfl_down(b_cur, 1);
+        const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
+        const uint32_t b0 = __builtin_amdgcn_readlane(b_nxt, 0);
+        if (lane == 63) {
+            hc = c0;
+            hbad = b0;
+        }
+        // windows of this lane: positions pos .. pos+15
+        const int64_t pos = (t << kTileShift) + lane_off;
+        const int64_t dlo = ps - pos, dhi = pe - pos;
+        const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
+        const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
+        const uint32_t badw = smear<K>(b_cur | (hbad << 16));
+        const uint32_t W = ~badw & mhi & mlo & 0xFFFFu;
+        const bool full = __all(W == 0xFFFFu);
+        count_tile<K, R, P16>(c_cur, hc, W, full, h, lane, pc);
+        c_cur = c_nxt;
+        b_cur = b_nxt;
+        r_nxt = r_nn;
+    }
+}
+
+template <int K, int R, bool P16, class Idx, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
+    constexpr int NB = 1 << (2 * K);
+    constexpr int NW = P16 ? NB / 2 : NB * R;
+    constexpr int NWAVES = BLOCK / 64;
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t *h = smem;
+    uint32_t *misc = smem + NW;  // [0] spill count, [1],[2] first record (lo, hi)
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int w = blockIdx.x;
+    const Geom g = make_geom<Idx>(p);
+    const int64_t tb = g.T0 + (int64_t)w * g.tpw;
+    const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
+    int64_t slot0 = -1, slot1 = -1;
+
+    if (tb < te) {
+        const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
+        const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
+        if (tid == 0) {
+            // last record s with indices[s] <= R0 (records before it end before R0)
+            int64_t lo = 0, hi = p.n - 1;
+            if (rec_off<Idx>(p, 0) <= R0) {
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi + 1) >> 1;
+                    if (rec_off<Idx>(p, mid) <= R0) lo = mid;
+                    else hi = mid - 1;
+                }
+            }
+            misc[0] = 0u;
+            misc[1] = (uint32_t)lo;
+            misc[2] = (uint32_t)((uint64_t)lo >> 32);
+        }
+        for (int i = tid; i < NW; i += BLOCK) h[i] = 0u;
+        __syncthreads();
+        const int64_t s0 = (int64_t)((uint64_t)misc[1] | ((uint64_t)misc[2] << 32));
+
+        P16Ctx pc;
+        pc.h = h;
+        pc.spill_n = misc;
+        pc.spill = p.spill ? p.spill + (int64_t)w * p.spill_cap : nullptr;
+        pc.cap = p.spill_cap;
+
+        int npieces = 0;
+        for (int64_t s = s0; s < p.n; ++s) {
+            if (rec_off<Idx>(p, s) >= R1) break;
+            int64_t ca, ce;
+            record_windows<K, Idx>(p, g, s, ca, ce);
+            const int64_t ps = ca > R0 ? ca : R0;
+            const int64_t pe = ce < R1 ? ce : R1;
+            if (ps >= pe) continue;
+            pc.rec = s;
+            // this piece's tiles, split into contiguous per-wave runs
+            const int64_t tp0 = ps >> kTileShift;
+            const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
+            const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
+            const int64_t a0 = tp0 + (int64_t)wave * per;
+            const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
+            count_wave_range<K, R, P16>(p.data, a0, a1, ps, pe, g.rl, g.rh, h, lane, pc);
+            __syncthreads();
+            const bool entire = (ps == ca) && (pe == ce);
+            int slot = 0;
+            if (!entire) {
+                slot = (npieces == 0) ? 0 : 1;
+                if (slot == 0) slot0 = s;
+                else slot1 = s;
+            }
+            uint32_t *dst = p.slab + ((int64_t)w * 2 + slot) * NB;
+            if constexpr (P16) {
+                for (int i = tid; i < NW; i += BLOCK) {
+                    const uint32_t v = h[i];
+                    h[i] = 0u;
+                    if (entire) {
+                        p.sum[s + p.ld * (int64_t)i] = (int32_t)(v & 0xFFFFu);
+                        p.sum[s + p.ld * (int64_t)(i + NW)] = (int32_t)(v >> 16);
+                    } else {
+                        dst[i] = v & 0xFFFFu;
+                        dst[i + NW] = v >> 16;
+                    }
+                }
+            } else {
+                for (int c = tid; c < NB; c += BLOCK) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        v += h[c * R + r];
+                        h[c * R + r] = 0u;
+                    }
+                    if (entire) p.sum[s + p.ld * (int64_t)c] = (int32_t)v;
+                    else dst[c] = v;
+                }
+            }
+            ++npieces;
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        p.slot_rec[2 * w] = slot0;
+        p.slot_rec[2 * w + 1] = slot1;
+        if (p.spill_cnt) p.spill_cnt[w] = (tb < te) ? misc[0] : 0u;
+    }
+}
+
+// Records that span several workgroups: sum their slab slots.
+template <int K, class Idx>
+__global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
+    constexpr int NB = 1 << (2 * K);
+    constexpr int CB = (NB + 255) / 256;
+    const int64_t s = blockIdx.x / CB;
+    const int c = (int)(blockIdx.x % CB) * 256 + threadIdx.x;
+    if (s >= p.n || c >= NB) return;
+    const Geom g = make_geom<Idx>(p);
+    int64_t ca, ce;
+    record_windows<K, Idx>(p, g, s, ca, ce);
+    if (ce <= ca) {
+        p.sum[s + p.ld * (int64_t)c] = 0;
+        return;
+    }
+    const int64_t wf = ((ca >> kTileShift) - g.T0) / g.tpw;
+    const int64_t wlast = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
+    if (wf == wlast) return;  // written directly by the count kernel
+    uint32_t acc = 0;
+    for (int64_t w = wf; w <= wlast; ++w) {
+        if (p.slot_rec[2 * w] == s) acc += p.slab[(2 * w) * NB + c];
+        if (p.slot_rec[2 * w + 1] == s) acc += p.slab[(2 * w + 1) * NB + c];
+    }
+    p.sum[s + p.ld * (int64_t)c] = (int32_t)acc;
+}
+
+__global__ __launch_bounds__(256) void spill_apply_kernel(Params p) {
+    const int w = blockIdx.x;
+    uint32_t cnt = p.spill_cnt[w];
+    if (cnt > p.spill_cap) cnt = p.spill_cap;
+    const Spill *sp = p.spill + (int64_t)w * p.spill_cap;
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const Spill e = sp[i];
+        atomicAdd(&p.sum[e.rec + p.ld * (int64_t)e.code], e.amount);
+    }
+}
+
+// invalid[s] = (#windows of s in range) - sum over codes (the CPU path's bin 0).
+template <int K, class Idx>
+__global__ __launch_bounds__(256) void invalid_kernel(Params p) {
+    constexpr int NB = 1 << (2 * K);
+    const int64_t s = blockIdx.x;
+    if (s >= p.n) return;
+    int64_t acc = 0;
+    for (int c = threadIdx.x; c < NB; c += 256) acc += p.sum[s + p.ld * (int64_t)c];
+    __shared__ int64_t red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const Geom g = make_geom<Idx>(p);
+        int64_t ca, ce;
+        record_windows<K, Idx>(p, g, s, ca, ce);
+        const int64_t nw = ce > ca ? ce - ca : 0;
+        p.invalid[s] = (int32_t)(nw - red[0]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <int K>
+struct Cfg;
+// R = replicas of each 32-bit bin; BLOCK = threads per workgroup
+template <> struct Cfg<1> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<2> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<3> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<4> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<5> { static constexpr int R = 8, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<6> { static constexpr int R = 2, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<7> { static constexpr int R = 1, BLOCK = 512; static constexpr bool P16 = false; };
+template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = 1024; static constexpr bool P16 = true; };
+
+template <int K>
+constexpr size_t lds_bytes() {
+    return (Cfg<K>::P16 ? ((size_t)1 << (2 * K)) / 2 : ((size_t)1 << (2 * K)) * Cfg<K>::R) * 4 + 16;
+}
+
+struct DevInfo {
+    int cus = 0;
+    int occ[KMC_DENSE_MAX_K + 1][2] = {};  // [k][idx64]
+};
+
+std::mutex g_mu;
+std::vector<DevInfo> g_dev;
+
+thread_local hipEvent_t t_trace_before = nullptr;
+thread_local hipEvent_t t_trace_after = nullptr;
+
+template <int K, class Idx>
+void *kernel_ptr() {
+    return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, Cfg<K>::P16, Idx, Cfg<K>::BLOCK>);
+}
+
+template <int K, class Idx>
+int grid_size(int device, int &G) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_dev.size() <= device) g_dev.resize(device + 1);
+    DevInfo &d = g_dev[device];
+    if (d.cus == 0) {
+        int v = 0;
+        hipError_t e = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device);
+        if (e != hipSuccess) return (int)e;
+        d.cus = v;
+    }
+    const int ix = sizeof(Idx) == 8 ? 1 : 0;
+    if (d.occ[K][ix] == 0) {
+        const void *kp = kernel_ptr<K, Idx>();
+        hipError_t e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<K>());
+        if (e != hipSuccess) return (int)e;
+        int nb = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, Cfg<K>::BLOCK, lds_bytes<K>());
+        if (e != hipSuccess) return (int)e;
+        d.occ[K][ix] = nb > 0 ? nb : 1;
+    }
+    G = d.cus * d.occ[K][ix];
+    return 0;
+}
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct WsLayout {
+    size_t slot_rec, spill_cnt, slab, spill, total;
+};
+
+inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
+    WsLayout L;
+    const size_t nb = (size_t)1 << (2 * k);
+    size_t o = 0;
+    L.slot_rec = o;
+    o += align256((size_t)G * 2 * sizeof(int64_t));
+    L.spill_cnt = o;
+    o += align256((size_t)G * sizeof(uint32_t));
+    L.slab = o;
+    o += align256((size_t)G * 2 * nb * sizeof(uint32_t));
+    L.spill = o;
+    o += align256((size_t)G * spill_cap * sizeof(Spill));
+    L.total = o;
+    return L;
+}
+
+// Upper bound of the spill entries one workgroup can emit for `tiles` tiles:
+// each entry needs 65 536 increments of one 16-bit field (or pairs with one).
+inline uint32_t spill_cap_for(int64_t tiles_per_wg) {
+    const int64_t windows = tiles_per_wg * kTile;
+    return (uint32_t)(4 * (windows / 65536) + 64);
+}
+
+struct Plan {
+    int G;
+    uint32_t spill_cap;
+    WsLayout L;
+};
+
+template <int K, class Idx>
+int make_plan(int device, bool derive, int64_t wl, int64_t wh, Plan &pl) {
+    int G = 0;
+    int e = grid_size<K, Idx>(device, G);
+    if (e) return e;
+    pl.spill_cap = 0;
+    if (!derive) {
+        const int64_t tiles = wh > wl ? ((wh + kTile - 1) >> kTileShift) - (wl >> kTileShift) : 0;
+        if (tiles < G) G = tiles > 0 ? (int)tiles : 1;
+        const int64_t tpw = tiles > 0 ? (tiles + G - 1) / G : 1;
+        if (Cfg<K>::P16) pl.spill_cap = spill_cap_for(tpw);
+    }
+    pl.G = G;
+    pl.L = ws_layout(K, G, pl.spill_cap);
+    return 0;
+}
+
+// library-owned workspace, per device
+struct WsCache {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+std::vector<WsCache> g_ws;
+
+int cached_workspace(int device, size_t need, void **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_ws.size() <= device) g_ws.resize(device + 1);
+    WsCache &c = g_ws[device];
+    if (c.bytes < need) {
+        if (c.ptr) {
+            hipError_t e = hipFree(c.ptr);
+            if (e != hipSuccess) return (int)e;
+            c.ptr = nullptr;
+            c.bytes = 0;
+        }
+        hipError_t e = hipMalloc(&c.ptr, need);
+        if (e != hipSuccess) return KMC_ERR_NOMEM;
+        c.bytes = need;
+    }
+    *out = c.ptr;
+    return 0;
+}
+
+struct Request {
+    const char *data;
+    const void *indices;
+    int64_t n;
+    int32_t *sum;
+    int64_t ld;
+    int32_t *invalid;
+    bool derive;
+    int64_t wl, wh, rl, rh;
+    void *ws;
+    size_t ws_bytes;
+};
+
+template <int K, class Idx>
+int run_dense(const Request &q, hipStream_t st) {
+    int device = 0;
+    hipError_t he = hipGetDevice(&device);
+    if (he != hipSuccess) return (int)he;
+    bool derive = q.derive;
+    int64_t wl = q.wl, wh = q.wh, rl = q.rl, rh = q.rh;
+    if (derive && Cfg<K>::P16) {
+        // the packed layout sizes its spill area from the range: read it once
+        Idx ends[2];
+        he = hipMemcpyAsync(&ends[0], q.indices, sizeof(Idx), hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(&ends[1], (const Idx *)q.indices + q.n, sizeof(Idx), hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipStreamSynchronize(st);
+        if (he != hipSuccess) return (int)he;
+        wl = rl = (int64_t)ends[0];
+        wh = rh = (int64_t)ends[1];
+        derive = false;
+    }
+    Plan pl;
+    int e = make_plan<K, Idx>(device, derive, wl, wh, pl);
+    if (e) return e;
+    void *ws = q.ws;
+    if (ws == nullptr) {
+        e = cached_workspace(device, pl.L.total, &ws);
+        if (e) return e;
+    } else if (q.ws_bytes < pl.L.total) {
+        return KMC_ERR_WORKSPACE;
+    }
+    char *base = static_cast<char *>(ws);
+    Params p;
+    p.data = q.data;
+    p.indices = q.indices;
+    p.n = q.n;
+    p.sum = q.sum;
+    p.ld = q.ld;
+    p.invalid = q.invalid;
+    p.wl = wl;
+    p.wh = wh;
+    p.rl = rl;
+    p.rh = rh;
+    p.derive = derive ? 1 : 0;
+    p.G = pl.G;
+    p.slot_rec = reinterpret_cast<int64_t *>(base + pl.L.slot_rec);
+    p.spill_cnt = Cfg<K>::P16 ? reinterpret_cast<uint32_t *>(base + pl.L.spill_cnt) : nullptr;
+    p.slab = reinterpret_cast<uint32_t *>(base + pl.L.slab);
+    p.spill = Cfg<K>::P16 ? reinterpret_cast<Spill *>(base + pl.L.spill) : nullptr;
+    p.spill_cap = pl.spill_cap;
+
+    constexpr int NB = 1 << (2 * K);
+    if (t_trace_before) {
+        he = hipEventRecord(t_trace_before, st);
+        if (he != hipSuccess) return (int)he;
+    }
+    hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, Cfg<K>::P16, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
+                       dim3(Cfg<K>::BLOCK), lds_bytes<K>(), st, p);
+    he = hipGetLastError();
+    if (he != hipSuccess) return (int)he;
+    if (t_trace_after) {
+        he = hipEventRecord(t_trace_after, st);
+        if (he != hipSuccess) return (int)he;
+    }
+    const int64_t cb = (NB + 255) / 256;
+    hipLaunchKernelGGL((reduce_dense_kernel<K, Idx>), dim3((unsigned)(q.n * cb)), dim3(256), 0, st, p);
+    he = hipGetLastError();
+    if (he != hipSuccess) return (int)he;
+    if (Cfg<K>::P16) {
+        hipLaunchKernelGGL(spill_apply_kernel, dim3(pl.G), dim3(256), 0, st, p);
+        he = hipGetLastError();
+        if (he != hipSuccess) return (int)he;
+    }
+    if (q.invalid) {
+        hipLaunchKernelGGL((invalid_kernel<K, Idx>), dim3((unsigned)q.n), dim3(256), 0, st, p);
+        he = hipGetLastError();
+        if (he != hipSuccess) return (int)he;
+    }
+    return 0;
+}
+
+template <class Idx>
+int dispatch(int k, const Request &q, hipStream_t st) {
+    switch (k) {
+        case 1: return run_dense<1, Idx>(q, st);
+        case 2: return run_dense<2, Idx>(q, st);
+        case 3: return run_dense<3, Idx>(q, st);
+        case 4: return run_dense<4, Idx>(q, st);
+        case 5: return run_dense<5, Idx>(q, st);
+        case 6: return run_dense<6, Idx>(q, st);
+        case 7: return run_dense<7, Idx>(q, st);
+        case 8: return run_dense<8, Idx>(q, st);
+        default: return KMC_ERR_UNSUPPORTED_K;
+    }
+}
+
+template <class Idx>
+size_t workspace_for(int k, int device, bool derive, int64_t wl, int64_t wh) {
+    Plan pl;
+    int e = 0;
+    switch (k) {
+        case 1: e = make_plan<1, Idx>(device, derive, wl, wh, pl); break;
+        case 2: e = make_plan<2, Idx>(device, derive, wl, wh, pl); break;
+        case 3: e = make_plan<3, Idx>(device, derive, wl, wh, pl); break;
+        case 4: e = make_plan<4, Idx>(device, derive, wl, wh, pl); break;
+        case 5: e = make_plan<5, Idx>(device, derive, wl, wh, pl); break;
+        case 6: e = make_plan<6, Idx>(device, derive, wl, wh, pl); break;
+        case 7: e = make_plan<7, Idx>(device, derive, wl, wh, pl); break;
+        case 8: e = make_plan<8, Idx>(device, derive, wl, wh, pl); break;
+        default: return 0;
+    }
+    return e ? 0 : pl.L.total;
+}
+
+}  // namespace
+}  // namespace kmc
+
+using namespace kmc;
+
+extern "C" int kmc_trace_set_events(hipEvent_t before, hipEvent_t after) {
+    t_trace_before = before;
+    t_trace_after = after;
+    return KMC_OK;
+}
+
+extern "C" int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_seqs, int *sum,
+                                                    hipStream_t stream) {
+    if (num_seqs == 0) return KMC_OK;
+    if (!data || !indices || !sum) return KMC_ERR_INVALID_ARG;
+    if (reinterpret_cast<uintptr_t>(data) & 15u) return KMC_ERR_ALIGNMENT;
+    Request q{};
+    q.data = data;
+    q.indices = indices;
+    q.n = num_seqs;
+    q.sum = sum;
+    q.ld = num_seqs;
+    q.derive = true;
+    return dispatch<int>(KMC_DROPIN_K, q, stream);
+}
+
+extern "C" size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *a, int device) {
+    if (!a || a->k < 1 || a->k > KMC_DENSE_MAX_K) return 0;
+    const int64_t wl = (int64_t)a->win_lo, wh = (int64_t)a->win_hi;
+    return workspace_for<int64_t>(a->k, device, false, wl, wh);
+}
+
+extern "C" int kmc_count_dense_ex(const kmc_dense_args *a, hipStream_t stream) {
+    if (!a) return KMC_ERR_INVALID_ARG;
+    if (a->k < 1 || a->k > KMC_DENSE_MAX_K) return KMC_ERR_UNSUPPORTED_K;
+    if (a->num_seqs == 0) return KMC_OK;
+    if (!a->data || !a->indices || !a->sum) return KMC_ERR_INVALID_ARG;
+    if (reinterpret_cast<uintptr_t>(a->data) & 15u) return KMC_ERR_ALIGNMENT;
+    if (a->read_hi < a->read_lo || a->win_hi < a->win_lo) return KMC_ERR_INVALID_ARG;
+    if (a->sum_ld != 0 && a->sum_ld < a->num_seqs) return KMC_ERR_INVALID_ARG;
+    Request q{};
+    q.data = a->data;
+    q.indices = a->indices;
+    q.n = (int64_t)a->num_seqs;
+    q.sum = a->sum;
+    q.ld = a->sum_ld ? (int64_t)a->sum_ld : (int64_t)a->num_seqs;
+    q.invalid = a->invalid;
+    q.derive = false;
+    q.wl = (int64_t)a->win_lo;
+    q.wh = (int64_t)a->win_hi;
+    q.rl = (int64_t)a->read_lo;
+    q.rh = (int64_t)a->read_hi;
+    q.ws = a->workspace;
+    q.ws_bytes = a->workspace_bytes;
+    return dispatch<int64_t>(a->k, q, stream);
+}
+
+extern "C" size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device) {
+    (void)num_seqs;
+    if (k < 1 || k > KMC_DENSE_MAX_K) return 0;
+    return workspace_for<int64_t>(k, device, false, 0, (int64_t)data_bytes);
+}
+
+extern "C" int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,
+                               int k, int32_t *sum, int32_t *invalid, void *workspace, size_t workspace_bytes,
+                               hipStream_t stream) {
+    kmc_dense_args a{};
+    a.data = data;
+    a.indices = indices;
+    a.num_seqs = num_seqs;
+    a.k = k;
+    a.sum = sum;
+    a.sum_ld = num_seqs;
+    a.invalid = invalid;
+    a.read_lo = 0;
+    a.read_hi = data_bytes;
+    a.win_lo = 0;
+    a.win_hi = data_bytes;
+    a.workspace = workspace;
+    a.workspace_bytes = workspace_bytes;
+    return kmc_count_dense_ex(&a, stream);
+}

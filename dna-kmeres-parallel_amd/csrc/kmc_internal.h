@@ -1,0 +1,14 @@
+// kmc_internal.h — declarations shared by the translation units of libkmc.so.
+#pragma once
+#include <cstdint>
+
+namespace kmc {
+// splitmix64 output n (0-based) of the stream seeded with `seed` (Steele et al.):
+// z = seed + (n+1)*golden; two xor-shift-multiply rounds; final xor-shift.
+__host__ __device__ inline uint64_t splitmix64_at(uint64_t seed, uint64_t n) {
+    uint64_t z = seed + (n + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+}  // namespace kmc

@@ -1,0 +1,252 @@
+"""kmc.py — Python binding of libkmc.so (the C ABI in include/kmc.h).
+
+The product is the HIP/C++ library; this module only marshals pointers for the
+tests, the benchmark and Python callers.  Device buffers are torch tensors
+(PyTorch is the allocator/stream provider here, nothing else).  There is no CPU
+fallback: every entry point raises if libkmc.so is missing or a call fails.
+
+Reference interface mirrored (axlwild/dna-kmeres-parallel):
+    sumKmereCoincidencesGlobalMemory(data, indices, num_seqs, sum)  kernels.h:113
+        -> dropin_count(data, indices_i32, num_seqs)
+    permutationsCountAll generalised to any k, GPU layout           main.cu:636-646
+        -> count_dense(data, indices, k)
+    importSeqs / importSeqsNoNL                                     main.cu:474-545 / 401-473
+        -> load_fasta(path, dialect)
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libkmc.so")
+HEADER = os.path.join(REPO, "include", "kmc.h")
+
+DIALECT_BLANK = 0  # importSeqs
+DIALECT_NONL = 1   # importSeqsNoNL
+MAX_SEQS_REFERENCE = 100
+DROPIN_K = 3
+
+
+class KmcError(RuntimeError):
+    def __init__(self, code, what):
+        self.code = code
+        super().__init__("%s failed: %s (%d)" % (what, error_string(code), code))
+
+
+_P = ctypes.c_void_p
+_U64 = ctypes.c_uint64
+_I64 = ctypes.c_int64
+
+
+class DenseArgs(ctypes.Structure):
+    _fields_ = [
+        ("data", _P), ("indices", _P), ("num_seqs", _U64), ("k", ctypes.c_int),
+        ("sum", _P), ("sum_ld", _U64), ("invalid", _P),
+        ("read_lo", _U64), ("read_hi", _U64), ("win_lo", _U64), ("win_hi", _U64),
+        ("workspace", _P), ("workspace_bytes", ctypes.c_size_t),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load libkmc.so (built in-tree by `make -C dna-kmeres-parallel_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libkmc.so not built: run `make -C %s` (no CPU fallback exists)" % HERE)
+        L = ctypes.CDLL(LIB_PATH)
+        L.kmc_error_string.restype = ctypes.c_char_p
+        L.kmc_error_string.argtypes = [ctypes.c_int]
+        L.kmc_version.restype = ctypes.c_int
+        L.sumKmereCoincidencesGlobalMemory_hip.argtypes = [_P, _P, ctypes.c_uint, _P, _P]
+        L.kmc_count_dense_workspace_size.restype = ctypes.c_size_t
+        L.kmc_count_dense_workspace_size.argtypes = [ctypes.c_int, _U64, _U64, ctypes.c_int]
+        L.kmc_count_dense.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, _P, _P, _P, ctypes.c_size_t, _P]
+        L.kmc_count_dense_ex.argtypes = [ctypes.POINTER(DenseArgs), _P]
+        L.kmc_count_dense_ex_workspace_size.restype = ctypes.c_size_t
+        L.kmc_count_dense_ex_workspace_size.argtypes = [ctypes.POINTER(DenseArgs), ctypes.c_int]
+        L.kmc_trace_set_events.argtypes = [_P, _P]
+        L.kmc_synth_fill.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
+        L.kmc_synth_indices.argtypes = [_P, _U64, _U64]
+        L.kmc_synth_indices.restype = None
+        L.kmc_fasta_load.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P)]
+        for fn in ("kmc_fasta_num_seqs", "kmc_fasta_data_bytes", "kmc_fasta_reference_num_indexes"):
+            getattr(L, fn).restype = _U64
+            getattr(L, fn).argtypes = [_P]
+        L.kmc_fasta_indices.restype = _P
+        L.kmc_fasta_indices.argtypes = [_P]
+        L.kmc_fasta_data.restype = _P
+        L.kmc_fasta_data.argtypes = [_P]
+        L.kmc_fasta_free.argtypes = [_P]
+        L.kmc_fasta_free.restype = None
+        _lib = L
+    return _lib
+
+
+def error_string(code):
+    return lib().kmc_error_string(int(code)).decode()
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise KmcError(rc, what)
+
+
+def header_symbols(path=HEADER):
+    """Function names declared by include/kmc.h."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", txt, flags=re.M)
+    return sorted(set(n for n in names if n not in ("defined",)))
+
+
+# ---------------------------------------------------------------------------
+# device entry points (torch tensors on cuda)
+# ---------------------------------------------------------------------------
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def dropin_count(data, indices, num_seqs=None, out=None, stream=None):
+    """Exact drop-in of the reference launch (k = 3): returns int32 sum[4^3 * n]
+    in the reference layout sum[s + n*code] (flat, like the reference)."""
+    import torch
+    n = int(num_seqs if num_seqs is not None else indices.numel() - 1)
+    if out is None:
+        out = torch.empty((1 << (2 * DROPIN_K)) * n, dtype=torch.int32, device=data.device)
+    rc = lib().sumKmereCoincidencesGlobalMemory_hip(_dptr(data), _dptr(indices), n, _dptr(out), _stream(stream))
+    _check(rc, "sumKmereCoincidencesGlobalMemory_hip")
+    return out
+
+
+def dense_workspace_size(k, num_seqs, data_bytes, device=0):
+    return int(lib().kmc_count_dense_workspace_size(k, num_seqs, data_bytes, device))
+
+
+def count_dense(data, indices, k, data_bytes=None, invalid=False, workspace=None, out=None, stream=None):
+    """k-mer histogram of every record: returns (sum (4^k, n) int32, invalid (n,) or None)."""
+    import torch
+    n = indices.numel() - 1
+    nb = 1 << (2 * k)
+    if data_bytes is None:
+        data_bytes = data.numel()
+    if out is None:
+        out = torch.empty((nb, n), dtype=torch.int32, device=data.device)
+    inv = torch.empty(n, dtype=torch.int32, device=data.device) if invalid else None
+    ws_ptr, ws_bytes = None, 0
+    if workspace is not None:
+        ws_ptr, ws_bytes = _dptr(workspace), workspace.numel() * workspace.element_size()
+    rc = lib().kmc_count_dense(_dptr(data), _dptr(indices), n, data_bytes, k, _dptr(out), _dptr(inv),
+                               ws_ptr, ws_bytes, _stream(stream))
+    _check(rc, "kmc_count_dense")
+    return out, inv
+
+
+def dense_args(data, indices, k, out, read=(0, None), win=(0, None), ld=0, invalid=None, workspace=None,
+               data_offset=0):
+    """Build a kmc_dense_args.  `data_offset` = global offset of data[0] (the data
+    pointer handed to the library is data_ptr - data_offset)."""
+    a = DenseArgs()
+    a.data = ctypes.c_void_p(data.data_ptr() - data_offset)
+    a.indices = ctypes.c_void_p(indices.data_ptr())
+    a.num_seqs = indices.numel() - 1
+    a.k = k
+    a.sum = ctypes.c_void_p(out.data_ptr())
+    a.sum_ld = ld
+    a.invalid = _dptr(invalid)
+    a.read_lo = read[0]
+    a.read_hi = read[1] if read[1] is not None else data_offset + data.numel()
+    a.win_lo = win[0]
+    a.win_hi = win[1] if win[1] is not None else data_offset + data.numel()
+    if workspace is not None:
+        a.workspace = ctypes.c_void_p(workspace.data_ptr())
+        a.workspace_bytes = workspace.numel() * workspace.element_size()
+    return a
+
+
+def count_dense_ex(args, stream=None):
+    rc = lib().kmc_count_dense_ex(ctypes.byref(args), _stream(stream))
+    _check(rc, "kmc_count_dense_ex")
+
+
+def dense_ex_workspace_size(args, device=0):
+    return int(lib().kmc_count_dense_ex_workspace_size(ctypes.byref(args), device))
+
+
+def trace_events(before=None, after=None):
+    """Record torch.cuda.Event `before`/`after` around the next dense count kernels."""
+    b = ctypes.c_void_p(before._as_parameter_.value) if before is not None else None
+    a = ctypes.c_void_p(after._as_parameter_.value) if after is not None else None
+    _check(lib().kmc_trace_set_events(b, a), "kmc_trace_set_events")
+
+
+def synth_fill(data, num_records, record_len, seed, first_base=0, stream=None):
+    rc = lib().kmc_synth_fill(_dptr(data), num_records, record_len, seed, first_base, _stream(stream))
+    _check(rc, "kmc_synth_fill")
+
+
+def synth_indices(num_records, record_len):
+    out = np.zeros(num_records + 1, dtype=np.int64)
+    lib().kmc_synth_indices(out.ctypes.data_as(_P), num_records, record_len)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# host: FASTA loader
+# ---------------------------------------------------------------------------
+def load_fasta(path, dialect=DIALECT_BLANK, max_seqs=MAX_SEQS_REFERENCE):
+    """Returns (data uint8, indices int64 [n+1], reference_num_indexes)."""
+    L = lib()
+    h = _P()
+    _check(L.kmc_fasta_load(os.fsencode(path), dialect, max_seqs, ctypes.byref(h)), "kmc_fasta_load")
+    try:
+        n = L.kmc_fasta_num_seqs(h)
+        nbytes = L.kmc_fasta_data_bytes(h)
+        idx = np.ctypeslib.as_array(ctypes.cast(L.kmc_fasta_indices(h), ctypes.POINTER(_I64)), (n + 1,)).copy()
+        if nbytes:
+            data = np.ctypeslib.as_array(ctypes.cast(L.kmc_fasta_data(h), ctypes.POINTER(ctypes.c_uint8)),
+                                         (nbytes,)).copy()
+        else:
+            data = np.zeros(0, dtype=np.uint8)
+        ref_n = L.kmc_fasta_reference_num_indexes(h)
+    finally:
+        L.kmc_fasta_free(h)
+    return data, idx, int(ref_n)
+
+
+# ---------------------------------------------------------------------------
+# host reference of the synthetic generator (tests compare the kernel to it)
+# ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def splitmix64_np(seed, n):
+    """Outputs n of splitmix64 (numpy uint64 array in, array out)."""
+    n = np.asarray(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (n + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_host(num_records, record_len, seed, first_base=0):
+    """Same bytes as kmc_synth_fill, on the host (small sizes)."""
+    g = np.arange(num_records * record_len, dtype=np.uint64) + np.uint64(first_base)
+    words = splitmix64_np(seed, g >> np.uint64(5))
+    codes = ((words >> (np.uint64(2) * (g & np.uint64(31)))) & np.uint64(3)).astype(np.uint8)
+    bases = np.frombuffer(b"ACGT", dtype=np.uint8)[codes].reshape(num_records, record_len)
+    out = np.zeros((num_records, record_len + 1), dtype=np.uint8)
+    out[:, :record_len] = bases
+    return out.reshape(-1)

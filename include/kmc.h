@@ -1,0 +1,170 @@
+/*
+ * kmc.h — C ABI of the MI355X-native k-mer counter (libkmc.so).
+ *
+ * Drop-in boundary for the hot path of axlwild/dna-kmeres-parallel: the step-1
+ * launch of sumKmereCoincidencesGlobalMemory (kernels.h:113, launched at
+ * main.cu:290) and its host-side feeders.  Plain C: pointers, sizes and int
+ * error codes only (0 = success, hipError_t values pass through, library codes
+ * are >= 1000).  Every device entry point is asynchronous on the given stream
+ * and never calls exit().
+ *
+ * Count layout (identical to the reference, kernels.h:142): int32
+ * sum[s + ld*code] ("k-mer-major, record-minor"), ld = num_seqs unless stated,
+ * code = sum_p code(x[i+p]) * 4^p with A=0,C=1,G=2,T=3 (first base least
+ * significant: the bin order of permutation(), utils.h:21-50).  Windows holding
+ * any byte other than uppercase A/C/G/T are not counted (kernels.h:136-139);
+ * their number per record is the reference CPU path's bin 0 (main.cu:643-644)
+ * and is available through the optional `invalid` output.
+ *
+ * Records follow the reference's buffer convention (main.cu:474-545): record s
+ * occupies data[indices[s] .. indices[s+1]), whose last byte is a terminator;
+ * windows start at offsets 0 .. (indices[s+1]-indices[s]) - k - 1.
+ */
+#ifndef KMC_H
+#define KMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef KMC_HIP_STREAM_T_DEFINED
+#define KMC_HIP_STREAM_T_DEFINED
+typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedef */
+#endif
+
+/* Compile-time k of the exact drop-in entry point (the reference's K, kernels.h:11-15). */
+#ifndef KMC_DROPIN_K
+#define KMC_DROPIN_K 3
+#endif
+
+/* Largest k of the dense (4^k-bin) histogram path. */
+#define KMC_DENSE_MAX_K 8
+
+/* Reference loader cap (main.cu:30). */
+#define KMC_MAX_SEQS_REFERENCE 100
+
+enum kmc_status {
+    KMC_OK = 0,
+    KMC_ERR_INVALID_ARG = 1001,   /* null pointer, bad size, bad range */
+    KMC_ERR_UNSUPPORTED_K = 1002, /* k outside the supported range of the entry point */
+    KMC_ERR_ALIGNMENT = 1003,     /* data pointer not 16-byte aligned */
+    KMC_ERR_WORKSPACE = 1004,     /* caller workspace smaller than *_workspace_size() */
+    KMC_ERR_IO = 1005,            /* file cannot be opened/read */
+    KMC_ERR_NOMEM = 1006,         /* host or device allocation failed */
+    KMC_ERR_RCCL = 1007,          /* RCCL call failed */
+    KMC_ERR_NO_DEVICE = 1008      /* no HIP device visible */
+};
+
+/* Human-readable text for a kmc_status or hipError_t code (static storage). */
+const char *kmc_error_string(int code);
+
+/* Library version: major*10000 + minor*100 + patch. */
+int kmc_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Exact drop-in for the reference launch
+ *     sumKmereCoincidencesGlobalMemory<<<54018, PERMS_KMERES>>>(data, indices, num_seqs, sum)
+ * (kernels.h:113, main.cu:290).  Same arguments, same meaning, same layout:
+ *   data     device (or managed) bytes, '\0'-terminated records
+ *   indices  device (or managed) int[num_seqs + 1] record offsets
+ *   sum      device (or managed) int[4^KMC_DROPIN_K * num_seqs]; every entry
+ *            (s < num_seqs, code < 4^K) is overwritten
+ * k = KMC_DROPIN_K (3, like the reference).  No pattern table (c_perms) is
+ * needed: codes are computed arithmetically in the reference's bin order.
+ * Uses a library-owned device workspace (allocated on first use per device).
+ * Asynchronous on `stream` (0 = the null stream); the reference synchronises
+ * after the launch (main.cu:291), so should the caller. */
+int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_seqs, int *sum,
+                                         hipStream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* k-generic, 64-bit-offset dense counter: the generalisation the reference's CPU
+ * path (permutationsCountAll, main.cu:636-646) computes for any k, on the GPU.
+ *   data        device pointer, 16-byte aligned, readable for [0, data_bytes)
+ *   indices     device int64[num_seqs + 1]
+ *   k           1 .. KMC_DENSE_MAX_K
+ *   sum         device int32[4^k * num_seqs], overwritten (layout above)
+ *   invalid     optional device int32[num_seqs]: invalid windows (CPU bin 0)
+ *   workspace   device scratch of kmc_count_dense_workspace_size() bytes, or
+ *               NULL to use a library-owned buffer (not graph-capture safe).  */
+size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device);
+
+int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,
+                    int k, int32_t *sum, int32_t *invalid, void *workspace, size_t workspace_bytes,
+                    hipStream_t stream);
+
+/* Extended form used for sharding: counts only the windows whose start offset
+ * lies in [win_lo, win_hi), reading only data[read_lo, read_hi) (a shard plus its
+ * (k-1)-byte halo), and writes sum[s + sum_ld*code] for every record s (zeros for
+ * records with no window in range).  Sums of shards covering disjoint window
+ * ranges equal the unsharded counts. */
+typedef struct kmc_dense_args {
+    const char *data;        /* device; global byte p is data[p] (only [read_lo, read_hi) is read) */
+    const int64_t *indices;  /* device int64[num_seqs + 1], global offsets */
+    uint64_t num_seqs;
+    int k;
+    int32_t *sum;            /* device */
+    uint64_t sum_ld;         /* row stride of sum (>= num_seqs); 0 -> num_seqs */
+    int32_t *invalid;        /* optional device int32[num_seqs] */
+    uint64_t read_lo, read_hi;
+    uint64_t win_lo, win_hi;
+    void *workspace;
+    size_t workspace_bytes;
+} kmc_dense_args;
+
+size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *args, int device);
+int kmc_count_dense_ex(const kmc_dense_args *args, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Tracing (the reference times step 1 with cudaEvents, main.cu:262-300): when set,
+ * every following dense count call on this host thread records `before` right
+ * before its histogram kernel and `after` right after it, on the call's stream,
+ * so the caller can time the hot kernel alone.  NULL, NULL switches it off. */
+#ifndef KMC_HIP_EVENT_T_DEFINED
+#define KMC_HIP_EVENT_T_DEFINED
+typedef struct ihipEvent_t *hipEvent_t; /* identical to HIP's own typedef */
+#endif
+int kmc_trace_set_events(hipEvent_t before, hipEvent_t after);
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic input generator (benchmark layout): num_records
+ * records of record_len bases, each followed by one '\0'; base g (global index
+ * first_base + r*record_len + i) is "ACGT"[(x_{g/32} >> 2*(g%32)) & 3] where x_n
+ * is output n of splitmix64 seeded with `seed`.  Writes num_records*(record_len+1)
+ * bytes.  kmc_synth_indices fills the matching int64 offsets on the host. */
+int kmc_synth_fill(char *data, uint64_t num_records, uint64_t record_len, uint64_t seed,
+                   uint64_t first_base, hipStream_t stream);
+void kmc_synth_indices(int64_t *indices, uint64_t num_records, uint64_t record_len);
+
+/* ------------------------------------------------------------------------ */
+/* FASTA loader (host), the successor of importSeqs / importSeqsNoNL
+ * (main.cu:474-545 / 401-473) with identical record semantics, int64 offsets
+ * and a streaming parser.
+ *   dialect 0 = importSeqs: records end at a blank or '\r'-initial line (a '>'
+ *               inside a record is sequence text);
+ *   dialect 1 = importSeqsNoNL: records also end at a '>' header line.
+ *   max_seqs  = the reference's MAX_SEQS cap (KMC_MAX_SEQS_REFERENCE keeps its
+ *               behaviour, including the 101st record); <= 0 means unlimited.
+ * The loaded buffer follows the reference convention ('|' bytes become '\0';
+ * each record ends with '\0') and always carries num_seqs + 1 offsets. */
+typedef struct kmc_fasta kmc_fasta;
+
+int kmc_fasta_load(const char *path, int dialect, int64_t max_seqs, kmc_fasta **out);
+uint64_t kmc_fasta_num_seqs(const kmc_fasta *f);
+const int64_t *kmc_fasta_indices(const kmc_fasta *f); /* num_seqs + 1 entries */
+const char *kmc_fasta_data(const kmc_fasta *f);
+uint64_t kmc_fasta_data_bytes(const kmc_fasta *f);
+/* Number of entries the reference's indexes_aux would hold: num_seqs + 1, or
+ * num_seqs when the input ends in a blank line (the reference then drops the end
+ * sentinel and its kernel reads out of bounds). */
+uint64_t kmc_fasta_reference_num_indexes(const kmc_fasta *f);
+void kmc_fasta_free(kmc_fasta *f);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KMC_H */

@@ -1,0 +1,45 @@
+"""Shared test setup: import paths, the `gpu` marker, in-tree builds."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "dna-kmeres-parallel_amd")
+ORACLE = os.path.join(REPO, "oracle")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (PKG, ORACLE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+    # build the in-tree libraries once if a fresh checkout lacks them (make is a no-op otherwise)
+    if not os.path.exists(os.path.join(PKG, "lib", "libkmc.so")):
+        subprocess.run(["make", "-s", "-j8", "-C", PKG], check=True)
+    if not os.path.exists(os.path.join(ORACLE, "libkmc_oracle.so")):
+        subprocess.run(["make", "-s", "-C", ORACLE, "all"], check=True)
+    if os.path.isdir("/root/reference") and not os.path.exists(os.path.join(ORACLE, "_ref", "libref_cpu.so")):
+        subprocess.run(["make", "-s", "-C", ORACLE, "ref"], check=True)
+
+
+@pytest.fixture(scope="session")
+def kmc():
+    import kmc as _kmc
+    return _kmc
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as _oracle
+    return _oracle
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test collected on a machine without a visible HIP device")
+    return torch.device("cuda:0")

@@ -1,0 +1,221 @@
+"""GPU parity of the HIP dense counter against the oracle and the reference kernel.
+
+Bit-exact integer comparisons throughout.  Run on the MI355X box (`-m gpu`).
+"""
+import numpy as np
+import pytest
+
+import golden_util as G
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).to(cuda)
+
+
+def random_records(rng, lens, n_frac=0.0, lower_frac=0.0, other_frac=0.0):
+    recs = []
+    for L in lens:
+        s = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=int(L))
+        if n_frac:
+            s[rng.random(s.size) < n_frac] = ord("N")
+        if lower_frac:
+            m = rng.random(s.size) < lower_frac
+            s[m] |= 0x20
+        if other_frac:
+            m = rng.random(s.size) < other_frac
+            s[m] = rng.integers(0, 256, size=int(m.sum()), dtype=np.uint8)
+        recs.append(np.append(s, np.uint8(0)))
+    data = np.concatenate(recs) if recs else np.zeros(0, np.uint8)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    return data, idx
+
+
+def run_dense(kmc, cuda, data, idx, k, **kw):
+    import torch
+    d = dev(data if data.size else np.zeros(16, np.uint8), cuda)
+    out, inv = kmc.count_dense(d, dev(idx, cuda), k, data_bytes=data.size, invalid=True, **kw)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), inv.cpu().numpy()
+
+
+def test_synth_kernel_matches_host(kmc, cuda):
+    import torch
+    for nrec, L, first in ((3, 1000, 0), (5, 4093, 17), (1, 65, 1 << 33)):
+        total = nrec * (L + 1)
+        buf = torch.zeros(total + 64, dtype=torch.uint8, device=cuda)
+        kmc.synth_fill(buf, nrec, L, 0x5EED0008, first)
+        torch.cuda.synchronize()
+        got = buf[:total].cpu().numpy()
+        np.testing.assert_array_equal(got, kmc.synth_host(nrec, L, 0x5EED0008, first))
+        assert int(buf[total:].sum()) == 0  # nothing written past the end
+
+
+@pytest.mark.parametrize("name,dialect", G.cases())
+def test_dense_matches_golden(kmc, cuda, name, dialect):
+    g = G.load(name, dialect)
+    idx = G.full_indices(g)
+    for k in g["ks"]:
+        k = int(k)
+        if k > 8:
+            continue
+        got, inv = run_dense(kmc, cuda, g["data"], idx, k)
+        exp, exp_inv = G.dense_expected(g, k)
+        np.testing.assert_array_equal(got, exp, err_msg="%s/%s k=%d" % (name, dialect, k))
+        np.testing.assert_array_equal(inv, exp_inv, err_msg="%s/%s k=%d invalid" % (name, dialect, k))
+
+
+@pytest.mark.parametrize("name", ["basic", "random", "maxseqs", "crlf", "odd"])
+def test_dropin_matches_golden(kmc, cuda, name):
+    import torch
+    g = G.load(name, "blank")
+    idx = G.full_indices(g).astype(np.int32)
+    n = idx.size - 1
+    d = dev(g["data"], cuda)
+    out = kmc.dropin_count(d, dev(idx, cuda), n)
+    torch.cuda.synchronize()
+    exp, _ = G.dense_expected(g, 3)
+    np.testing.assert_array_equal(out.cpu().numpy().reshape(64, n), exp)
+
+
+def test_dropin_matches_reference_kernel(kmc, oracle, cuda):
+    """The reference's own sumKmereCoincidencesGlobalMemory (kernels.h, compiled for
+    gfx950 from /root/reference into oracle/_ref) vs the drop-in, same buffers."""
+    import torch
+    if not oracle.have_ref_kernel():
+        pytest.skip("oracle/_ref/libref_kernel.so not built")
+    L = oracle.ref_kernel()
+    assert L.ref_kernel_k() == 3
+    assert L.ref_kernel_upload_patterns() == 0
+    rng = np.random.default_rng(3)
+    for lens in ([5000, 1, 2, 3, 4, 777, 10000], list(rng.integers(0, 3000, size=101))):
+        data, idx = random_records(rng, lens, 0.01, 0.01, 0.002)
+        idx32 = idx.astype(np.int32)
+        n = idx.size - 1
+        d = dev(data, cuda)
+        di = dev(idx32, cuda)
+        ref = torch.zeros(64 * n, dtype=torch.int32, device=cuda)
+        assert L.ref_kernel_launch(d.data_ptr(), di.data_ptr(), n, ref.data_ptr()) == 0
+        ours = kmc.dropin_count(d, di, n)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(ours.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_dense_random_vs_oracle(kmc, oracle, cuda, k):
+    rng = np.random.default_rng(1000 + k)
+    # short, tile-straddling and multi-workgroup records; invalid bytes of every kind
+    lens = [0, 1, k - 1, k, k + 1, 15, 16, 17, 1023, 1024, 1025, 70000, 3, 250000, 4096 * 3 + 5]
+    data, idx = random_records(rng, lens, 0.003, 0.003, 0.001)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
+@pytest.mark.parametrize("k", [3, 8])
+def test_dense_long_records_span_workgroups(kmc, oracle, cuda, k):
+    """Records of several MB: every record is cut over many workgroups (slab reduce)."""
+    rng = np.random.default_rng(77)
+    data, idx = random_records(rng, [3_000_001, 2_500_000, 17, 4_000_003], 0.0005, 0.0005)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
+def test_k8_packed_counter_wraps(kmc, oracle, cuda):
+    """k = 8 keeps two 16-bit counters per LDS word: low-entropy input drives
+    both halves of the same words through many wraps concurrently."""
+    rng = np.random.default_rng(8)
+    n = 48 * 1024 * 1024
+    # 97 % A, 3 % G: bins 0 (AAAAAAAA, low half of word 0) and 0x8000 (AAAAAAAG, high
+    # half of word 0) and the other single-G bins each get millions of counts
+    s = np.where(rng.random(n) < 0.97, ord("A"), ord("G")).astype(np.uint8)
+    s[: 4 * 1024 * 1024] = ord("A")               # one long run: > 65 536 adds per workgroup
+    s[-3 * 1024 * 1024:] = np.frombuffer(b"AAAAAAAG", np.uint8)[np.arange(3 * 1024 * 1024) % 8]
+    data = np.append(s, np.uint8(0))
+    idx = np.array([0, data.size], dtype=np.int64)
+    got, inv = run_dense(kmc, cuda, data, idx, 8)
+    exp, exp_inv = oracle.count_dense(data, idx, 8)
+    assert exp[0, 0] > 1 << 21 and exp[0x8000, 0] > 1 << 17
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
+@pytest.mark.parametrize("k", [4, 8])
+def test_range_shards_sum_to_full(kmc, oracle, cuda, k):
+    """kmc_count_dense_ex over disjoint window ranges, each reading only its
+    shard + (k-1)-byte halo, sums to the unsharded histogram."""
+    import torch
+    rng = np.random.default_rng(5)
+    data, idx = random_records(rng, [100_000, 7, 300_000, 123_457], 0.001, 0.001)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    d = dev(data, cuda)
+    di = dev(idx, cuda)
+    cuts = [0, 4096, 4097, 150_003, 150_016, 400_000, data.size]
+    acc = np.zeros_like(exp)
+    inv_acc = np.zeros_like(exp_inv)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        out = torch.full((1 << (2 * k), idx.size - 1), -7, dtype=torch.int32, device=cuda)
+        inv = torch.full((idx.size - 1,), -7, dtype=torch.int32, device=cuda)
+        args = kmc.dense_args(d, di, k, out, read=(a, min(b + k - 1, data.size)), win=(a, b), invalid=inv)
+        kmc.count_dense_ex(args)
+        torch.cuda.synchronize()
+        part, pinv = out.cpu().numpy(), inv.cpu().numpy()
+        ref_part, ref_pinv = oracle.count_dense(data, idx, k, win=(a, b))
+        np.testing.assert_array_equal(part, ref_part)
+        np.testing.assert_array_equal(pinv, ref_pinv)
+        acc += part
+        inv_acc += pinv
+    np.testing.assert_array_equal(acc, exp)
+    np.testing.assert_array_equal(inv_acc, exp_inv)
+
+
+def test_sum_ld_column_block_and_workspace(kmc, oracle, cuda):
+    """Writing into columns [off, off+n) of a wider matrix (multi-rank layout),
+    with a caller-provided workspace."""
+    import torch
+    rng = np.random.default_rng(9)
+    data, idx = random_records(rng, [5000, 60000, 1], 0.01, 0.0)
+    n, k, ld, off = idx.size - 1, 6, 10, 4
+    big = torch.full((1 << (2 * k), ld), -1, dtype=torch.int32, device=cuda)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    flat = big.view(-1)[off:]
+    args = kmc.dense_args(d, di, k, flat, ld=ld)
+    ws_bytes = kmc.dense_ex_workspace_size(args)
+    assert ws_bytes > 0
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=cuda)
+    args = kmc.dense_args(d, di, k, flat, ld=ld, workspace=ws)
+    kmc.count_dense_ex(args)
+    torch.cuda.synchronize()
+    got = big.cpu().numpy()
+    exp, _ = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got[:, off:off + n], exp)
+    assert (got[:, :off] == -1).all() and (got[:, off + n:] == -1).all()
+    # too small a workspace is refused
+    small = kmc.dense_args(d, di, k, flat, ld=ld, workspace=ws[: ws_bytes // 2])
+    with pytest.raises(kmc.KmcError) as e:
+        kmc.count_dense_ex(small)
+    assert e.value.code == 1004
+
+
+def test_synthetic_1gbase_k8_full_parity(kmc, oracle, cuda):
+    """1 Gbase of the benchmark's own synthetic layout (4 x 250 Mbase), generated
+    on the GPU, counted at k = 8 and compared bin for bin with the oracle."""
+    import torch
+    nrec, L = 4, 250_000_000
+    total = nrec * (L + 1)
+    buf = torch.empty(total, dtype=torch.uint8, device=cuda)
+    kmc.synth_fill(buf, nrec, L, 0x5EED0008)
+    idx = kmc.synth_indices(nrec, L)
+    out, inv = kmc.count_dense(buf, dev(idx, cuda), 8, invalid=True)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    host = buf.cpu().numpy()
+    exp, exp_inv = oracle.count_dense(host, idx, 8)
+    np.testing.assert_array_equal(got, exp)
+    assert (inv.cpu().numpy() == 0).all() and (exp_inv == 0).all()
+    assert int(got.astype(np.int64).sum()) == nrec * (L - 8 + 1)

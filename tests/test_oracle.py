@@ -1,0 +1,79 @@
+"""The oracle (C restatement) pinned against the reference's own outputs."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_util as G
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5])
+def test_bin_order_matches_permutation(oracle, k):
+    """Pattern i of the reference's permutation() (utils.h:21-50) has LE code i."""
+    pats = np.load(os.path.join(G.GOLDEN, "patterns_k%d.npy" % k))
+    for i, row in enumerate(pats):
+        assert oracle.lib().oracle_window_code(row.tobytes(), k) == i
+
+
+@pytest.mark.parametrize("name,dialect", G.cases())
+def test_oracle_matches_golden(oracle, name, dialect):
+    g = G.load(name, dialect)
+    idx = G.full_indices(g)
+    for k in g["ks"]:
+        k = int(k)
+        got, inv = oracle.count_dense(g["data"], idx, k)
+        exp, exp_inv = G.dense_expected(g, k)
+        np.testing.assert_array_equal(got, exp, err_msg="%s/%s k=%d" % (name, dialect, k))
+        np.testing.assert_array_equal(inv, exp_inv)
+
+
+def _random_records(rng, n, lo, hi, n_frac=0.01, lower_frac=0.01):
+    recs = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi))
+        s = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=L)
+        s[rng.random(L) < n_frac] = ord("N")
+        m = rng.random(L) < lower_frac
+        s[m] |= 0x20
+        recs.append(np.append(s, np.uint8(0)))
+    data = np.concatenate(recs) if recs else np.zeros(0, np.uint8)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    return data, idx
+
+
+@pytest.mark.parametrize("k", [1, 3, 4, 7])
+def test_oracle_matches_python_restatement(oracle, k):
+    rng = np.random.default_rng(k)
+    data, idx = _random_records(rng, 6, 0, 300)
+    got, inv = oracle.count_dense(data, idx, k)
+    for s in range(idx.size - 1):
+        h = oracle.py_count_record(bytes(data[idx[s]:idx[s + 1]]), k)
+        assert h[0] == inv[s]
+        np.testing.assert_array_equal(got[:, s], h[1:])
+
+
+@pytest.mark.parametrize("k", [2, 3, 6, 8, 9])
+def test_oracle_matches_reference_live(oracle, k):
+    """Against the reference's permutationsCountAll compiled from /root/reference."""
+    if not oracle.have_ref_cpu():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(100 + k)
+    data, idx = _random_records(rng, 4, 1, 3000, 0.005, 0.005)
+    got, inv = oracle.count_dense(data, idx, k)
+    for s in range(idx.size - 1):
+        h = oracle.ref_count_bytes(data[idx[s]:idx[s + 1]], k)
+        assert h[0] == inv[s]
+        np.testing.assert_array_equal(got[:, s], h[1:])
+
+
+def test_oracle_range_partition_sums(oracle):
+    """Windowed counting over disjoint start ranges sums to the full count."""
+    rng = np.random.default_rng(7)
+    data, idx = _random_records(rng, 5, 0, 2000)
+    full, _ = oracle.count_dense(data, idx, 5)
+    cuts = [0, 100, 1000, 1001, 4096, data.size]
+    acc = np.zeros_like(full)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        part, _ = oracle.count_dense(data, idx, 5, win=(a, b))
+        acc += part
+    np.testing.assert_array_equal(acc, full)
