@@ -34,6 +34,21 @@
 #include "kmc.h"
 #include "kmc_internal.h"
 
+// Diagnostic builds only (scripts/kbench.py): KMC_ABLATE=1 replaces the LDS
+// histogram update by a register XOR (codes still computed), KMC_ABLATE=2 also
+// skips the decode (loads only).  The shipped library is built with KMC_ABLATE=0.
+#ifndef KMC_ABLATE
+#define KMC_ABLATE 0
+#endif
+// Tiles kept in flight per wave ahead of the one being counted, and whether the
+// once-read sequence stream uses non-temporal (nt) loads.
+#ifndef KMC_PF
+#define KMC_PF 2
+#endif
+#ifndef KMC_NT
+#define KMC_NT 0
+#endif
+
 namespace kmc {
 namespace {
 
@@ -61,6 +76,8 @@ struct Params {
     Spill *spill;            // [G][spill_cap]
     uint32_t *spill_cnt;     // [G]
     uint32_t spill_cap;
+    uint64_t *fail_mask;     // [G] HM 3: bit i = i-th piece of the workgroup overflowed (bit 63: any >= 63)
+    int fallback;            // 1: recount only the pieces flagged in fail_mask (exact HM 1 kernel)
 };
 
 struct Geom {
@@ -109,33 +126,74 @@ __device__ __forceinline__ void record_windows(const Params &p, const Geom &g, i
     ce = (a + nw) < g.wh ? (a + nw) : g.wh;
 }
 
-// 16 ASCII bytes -> 2-bit LE codes (A0 C1 G2 T3) and a 1-bit-per-base invalid mask.
-//   code(b) = ((b >> 1) ^ (b >> 2)) & 3 maps A,C,G,T to 0,1,2,3; a byte is valid iff
-//   it equals the canonical letter of its code (v_perm_b32 as a 4-entry table).
-__device__ __forceinline__ void pack16(const uint4 r, uint32_t &code, uint32_t &bad) {
-    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-    code = 0;
-    bad = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t c = ((w[d] >> 1) ^ (w[d] >> 2)) & 0x03030303u;
-        const uint32_t canon = __builtin_amdgcn_perm(0u, 0x54474341u, c);  // "ACGT"[c] per byte
-        const uint32_t x = w[d] ^ canon;
-        const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-        const uint32_t b4 = (((nz >> 7) * 0x00204081u) >> 21) & 0xFu;
-        const uint32_t q = c | (c >> 6);
-        const uint32_t p8 = (q & 0xFu) | ((q >> 12) & 0xF0u);
-        code |= p8 << (8 * d);
-        bad |= b4 << (4 * d);
-    }
+// ---------------------------------------------------------------------------
+// decode: 16 ASCII bytes (one lane's chunk) -> 32-bit word of 2-bit codes, base i
+// at bits 2i (the reference's little-endian bin order), plus validity.
+//
+// The low 3 bits of A,C,G,T are 1,3,7,4 and distinct, so one v_perm_b32 on
+// (w & 0x07070707) maps every byte to its code (a 4-entry table lookup per
+// byte) and a second one to the letter that code stands for; a byte is valid
+// iff it equals that letter (lowercase, N, '\r', '\0', ... never do).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kCodeLo = 0x01000000u;   // table[0..3] = {-, A=0, -, C=1}
+constexpr uint32_t kCodeHi = 0x02000003u;   // table[4..7] = {T=3, -, -, G=2}
+constexpr uint32_t kCanonLo = 0x43FF41FFu;  // table[0..3] = {xx, 'A', xx, 'C'}
+constexpr uint32_t kCanonHi = 0x47FFFF54u;  // table[4..7] = {'T', xx, xx, 'G'}
+
+__device__ __forceinline__ uint32_t byte_codes(uint32_t w) {
+    return __builtin_amdgcn_perm(kCodeHi, kCodeLo, w & 0x07070707u);
+}
+__device__ __forceinline__ uint32_t byte_mismatch(uint32_t w) {  // 0 in every valid byte
+    return w ^ __builtin_amdgcn_perm(kCanonHi, kCanonLo, w & 0x07070707u);
 }
 
-__device__ __forceinline__ uint4 load_chunk(const char *data, int64_t q, int64_t rl, int64_t rh) {
-    if (q >= rl && q + 16 <= rh) return *reinterpret_cast<const uint4 *>(data + q);
+// code = 16 packed 2-bit codes; bad = OR of the per-byte mismatches (0 iff all valid)
+__device__ __forceinline__ void decode16(const uint4 r, uint32_t &code, uint32_t &bad) {
+    const uint32_t c0 = byte_codes(r.x), c1 = byte_codes(r.y), c2 = byte_codes(r.z), c3 = byte_codes(r.w);
+    bad = byte_mismatch(r.x) | byte_mismatch(r.y) | byte_mismatch(r.z) | byte_mismatch(r.w);
+    // bytes -> nibbles -> one byte per dword (base 4d+i at bits 2(4d+i))
+    const uint32_t u = __builtin_amdgcn_perm(c1, c0, 0x06040200u) | (__builtin_amdgcn_perm(c1, c0, 0x07050301u) << 2);
+    const uint32_t v = __builtin_amdgcn_perm(c3, c2, 0x06040200u) | (__builtin_amdgcn_perm(c3, c2, 0x07050301u) << 2);
+    code = __builtin_amdgcn_perm(v, u, 0x06040200u) | (__builtin_amdgcn_perm(v, u, 0x07050301u) << 4);
+}
+
+// 16-bit invalid-base mask of a chunk (slow path only)
+__device__ __forceinline__ uint32_t bad_mask16(const uint4 r) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    uint32_t bad = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t x = byte_mismatch(w[d]);
+        const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        bad |= ((((nz >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * d);
+    }
+    return bad;
+}
+
+// One lane's 16 bytes of tile t; bytes outside [rl, rh) read as 0 (invalid).
+__device__ __forceinline__ uint4 load_lane(const char *__restrict__ data, int64_t t, int lane, int64_t rl,
+                                           int64_t rh) {
+    const int64_t base = t << kTileShift;
+    const int64_t q = base + (int64_t)lane * 16;
+    if (base >= rl && base + kTile <= rh) {  // wave-uniform: whole tile readable
+#if KMC_NT
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(data + q));
+        return make_uint4(x[0], x[1], x[2], x[3]);
+#else
+        return *reinterpret_cast<const uint4 *>(data + q);
+#endif
+    }
     uint32_t v[4] = {0u, 0u, 0u, 0u};
-    for (int i = 0; i < 16; ++i) {
-        const int64_t b = q + i;
-        if (b >= rl && b < rh) v[i >> 2] |= (uint32_t)(uint8_t)data[b] << (8 * (i & 3));
+    if (q >= rl && q + 16 <= rh) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(data + q);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else {
+#pragma unroll 1
+        for (int i = 0; i < 16; ++i) {
+            const int64_t b = q + i;
+            if (b >= rl && b < rh) v[i >> 2] |= (uint32_t)(uint8_t)data[b] << (8 * (i & 3));
+        }
     }
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
@@ -196,61 +254,94 @@ __device__ __noinline__ void p16_fix(const P16Ctx &c, uint32_t word, uint32_t hb
     }
 }
 
-// Count the windows of one tile for one lane.  lo = codes of the lane's 16 bases,
-// hi = codes of the next 16 (halo), W = 16-bit mask of windows to count.
-template <int K, int R, bool P16>
-__device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W, bool full, uint32_t *h,
-                                           int lane, const P16Ctx &pc) {
+// Code of window j (0..15) of a lane whose bases are lo (own 16) : hi (next 16).
+template <int K, int J>
+__device__ __forceinline__ uint32_t window_code(uint32_t lo, uint32_t mid) {
+    constexpr uint32_t M = (K == 16) ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
+    if constexpr (J <= 16 - K)
+        return (lo >> (2 * J)) & M;
+    else
+        return (mid >> (2 * (J - 8))) & M;
+}
+
+template <int K, int R, int J, bool MASKED>
+__device__ __forceinline__ void add32(uint32_t lo, uint32_t mid, uint32_t W, uint32_t *h, uint32_t rep) {
+    const uint32_t code = window_code<K, J>(lo, mid);
+    if (!MASKED || ((W >> J) & 1u))
+        __hip_atomic_fetch_add(&h[code * R + rep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int K, int R, bool MASKED>
+__device__ __forceinline__ void count_tile32(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h, int lane) {
     const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);  // bases 8..23
-    if constexpr (!P16) {
-        const uint32_t rep = (uint32_t)(lane & (R - 1));
-        if (full) {
+    const uint32_t rep = (uint32_t)(lane & (R - 1));
+    add32<K, R, 0, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 1, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 2, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 3, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 4, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 5, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 6, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 7, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 8, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 9, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 10, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 11, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 12, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 13, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 14, MASKED>(lo, mid, W, h, rep);
+    add32<K, R, 15, MASKED>(lo, mid, W, h, rep);
+}
+
+// k == 8, packed 16-bit halves with returning adds (HM == 1).  The 16 adds of a
+// tile are issued, and their returned values are checked one tile later
+// (p16_check), so the LDS return latency hides behind the next tile's decode.
+struct P16Pending {
+    uint32_t old[16];
+    uint32_t lo, hi, W;
+};
+
+template <bool MASKED>
+__device__ __forceinline__ void count_tile_p16(uint32_t lo, uint32_t hi, uint32_t W, const P16Ctx &pc,
+                                               P16Pending &pd) {
+    const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                uint32_t code;
-                if (j <= 16 - K) code = (lo >> (2 * j)) & ((1u << (2 * K)) - 1u);
-                else code = (mid >> (2 * (j - 8))) & ((1u << (2 * K)) - 1u);
-                __hip_atomic_fetch_add(&h[code * R + rep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        } else {
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t src = (j <= 8) ? lo : mid;
+        const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
+        const uint32_t word = (src >> off) & 0x7FFFu;
+        const uint32_t hb = (src >> (off + 15)) & 1u;
+        pd.old[j] = 0u;
+        if (!MASKED || ((W >> j) & 1u))
+            pd.old[j] = __hip_atomic_fetch_add(&pc.h[word], hb * 0xFFFFu + 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    pd.lo = lo;
+    pd.hi = hi;
+    pd.W = MASKED ? W : 0xFFFFu;
+}
+
+// Conservative precheck: a half can only have wrapped if some returned value had
+// a half >= 0x8000; random input never gets there, skewed input takes the exact
+// per-window path.
+__device__ __forceinline__ void p16_check(const P16Ctx &pc, const P16Pending &pd) {
+    uint32_t any = 0u;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                uint32_t code;
-                if (j <= 16 - K) code = (lo >> (2 * j)) & ((1u << (2 * K)) - 1u);
-                else code = (mid >> (2 * (j - 8))) & ((1u << (2 * K)) - 1u);
-                if ((W >> j) & 1u)
-                    __hip_atomic_fetch_add(&h[code * R + rep], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        }
-    } else {
-        static_assert(K == 8, "packed 16-bit histogram is the k == 8 layout");
-        uint32_t old[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t src = (j <= 8) ? lo : mid;
-            const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
-            const uint32_t word = (src >> off) & 0x7FFFu;
-            const uint32_t hb = (src >> (off + 15)) & 1u;
-            const uint32_t inc = hb ? 0x10000u : 1u;
-            old[j] = 0u;
-            if (full || ((W >> j) & 1u))
-                old[j] = __hip_atomic_fetch_add(&h[word], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        // checks after all 16 adds are in flight (LDS returns in order: counted waits)
+    for (int j = 0; j < 16; ++j) any |= pd.old[j];
+    if (__any((any & 0x80008000u) != 0u)) {
+        const uint32_t mid = __builtin_amdgcn_alignbit(pd.hi, pd.lo, 16);
         uint32_t ovf = 0u, hw = 0u;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const uint32_t src = (j <= 8) ? lo : mid;
+            const uint32_t src = (j <= 8) ? pd.lo : mid;
             const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
-            const uint32_t hb = (src >> (off + 15)) & 1u;
-            const uint32_t m = hb ? 0xFFFF0000u : 0x0000FFFFu;
-            ovf |= (uint32_t)((old[j] & m) == m) << j;
-            hw |= (uint32_t)(old[j] >= 0xFFFF0000u) << j;
+            const uint32_t m = ((src >> (off + 15)) & 1u) ? 0xFFFF0000u : 0x0000FFFFu;
+            ovf |= (uint32_t)((pd.old[j] & m) == m) << j;
+            hw |= (uint32_t)(pd.old[j] >= 0xFFFF0000u) << j;
         }
-        if (!full) ovf &= W;
-        if (__any(ovf != 0u)) {
-            const uint64_t both = (uint64_t)lo | ((uint64_t)hi << 32);
+        ovf &= pd.W;
+        if (ovf != 0u) {
+            const uint64_t both = (uint64_t)pd.lo | ((uint64_t)pd.hi << 32);
             for (int j = 0; j < 16; ++j) {
                 if ((ovf >> j) & 1u) {
                     const uint32_t code = (uint32_t)(both >> (2 * j)) & 0xFFFFu;
@@ -261,59 +352,213 @@ __device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W,
     }
 }
 
-// One wave counts the windows of tiles [t0, t1) that start in [ps, pe).
-template <int K, int R, bool P16>
-__device__ void count_wave_range(const char *data, int64_t t0, int64_t t1, int64_t ps, int64_t pe, int64_t rl,
-                                 int64_t rh, uint32_t *h, int lane, const P16Ctx &pc) {
-    if (t0 >= t1) return;
-    const int64_t lane_off = (int64_t)lane * 16;
-    uint4 r_nxt = load_chunk(data, ((t0 + 1) << kTileShift) + lane_off, rl, rh);
-    uint32_t c_cur, b_cur;
-    pack16(load_chunk(data, (t0 << kTileShift) + lane_off, rl, rh), c_cur, b_cur);
-    for (int64_t t = t0; t < t1; ++t) {
-        uint4 r_nn = make_uint4(0u, 0u, 0u, 0u);
-        if (t + 2 <= t1) r_nn = load_chunk(data, ((t + 2) << kTileShift) + lane_off, rl, rh);
-        uint32_t c_nxt, b_nxt;
-        pack16(r_nxt, c_nxt, b_nxt);
-        // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
-        uint32_t hc = __shfl_down(c_cur, 1);
-        uint32_t hbad = __shfl_down(b_cur, 1);
-        const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
-        const uint32_t b0 = __builtin_amdgcn_readlane(b_nxt, 0);
-        if (lane == 63) {
-            hc = c0;
-            hbad = b0;
-        }
-        // windows of this lane: positions pos .. pos+15
-        const int64_t pos = (t << kTileShift) + lane_off;
-        const int64_t dlo = ps - pos, dhi = pe - pos;
-        const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
-        const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
-        const uint32_t badw = smear<K>(b_cur | (hbad << 16));
-        const uint32_t W = ~badw & mhi & mlo & 0xFFFFu;
-        const bool full = __all(W == 0xFFFFu);
-        count_tile<K, R, P16>(c_cur, hc, W, full, h, lane, pc);
-        c_cur = c_nxt;
-        b_cur = b_nxt;
-        r_nxt = r_nn;
+// k == 8, packed 16-bit halves, plain adds (HM == 2): overflow is excluded by the
+// between-barrier scans of count_wave_range (p16_scan).
+template <bool MASKED>
+__device__ __forceinline__ void count_tile_p16_plain(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h) {
+    const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t src = (j <= 8) ? lo : mid;
+        const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
+        const uint32_t word = (src >> off) & 0x7FFFu;
+        const uint32_t hb = (src >> (off + 15)) & 1u;
+        if (!MASKED || ((W >> j) & 1u))
+            __hip_atomic_fetch_add(&h[word], hb * 0xFFFFu + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
-template <int K, int R, bool P16, class Idx, int BLOCK>
+template <int K, int R, int HM, bool MASKED>
+__device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h, int lane,
+                                           const P16Ctx &pc, P16Pending &pd) {
+#if KMC_ABLATE == 1
+    const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x ^= (j <= 16 - K) ? (lo >> (2 * j)) : (mid >> (2 * (j - 8)));
+    asm volatile("" ::"v"(x), "v"(W));
+#elif KMC_ABLATE == 2
+    asm volatile("" ::"v"(lo), "v"(hi), "v"(W));
+#else
+    if constexpr (HM == 1)
+        count_tile_p16<MASKED>(lo, hi, W, pc, pd);
+    else if constexpr (HM == 2 || HM == 3)
+        count_tile_p16_plain<MASKED>(lo, hi, W, h);
+    else
+        count_tile32<K, R, MASKED>(lo, hi, W, h, lane);
+#endif
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for
+// the wave's outstanding global loads, so the tile prefetch keeps streaming.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// HM == 2 overflow scans.  Between two scans the workgroup adds at most
+// NWAVES*ScanTiles<BLOCK>*1024 windows (each wave ScanTiles tiles); a scan moves
+// every 16-bit half >= T down to (half mod T), the rest going to a spill entry.
+// With NWAVES*ScanTiles*1024 <= 65536 - T a half is < T after a scan and
+// <= 65535 before the next one: no half ever wraps.
+template <int BLOCK> struct Scan;
+template <> struct Scan<1024> { static constexpr int kTiles = 3; static constexpr uint32_t kT = 16384; };
+template <> struct Scan<512> { static constexpr int kTiles = 7; static constexpr uint32_t kT = 8192; };
+
+// Cold path of the scan: move every half's multiple of T of 4 words into spills.
+template <uint32_t T>
+__device__ __noinline__ void p16_scan_fix(const P16Ctx &pc, int i4) {
+    uint32_t *w = pc.h + 4 * i4;
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t word = (uint32_t)(4 * i4 + q);
+        const uint32_t x = w[q];
+        const uint32_t lo = x & 0xFFFFu, hi = x >> 16;
+        if (lo >= T) p16_spill(pc, (int32_t)word, (int32_t)(lo & ~(T - 1)));
+        if (hi >= T) p16_spill(pc, (int32_t)(word | 0x8000u), (int32_t)(hi & ~(T - 1)));
+        w[q] = (lo & (T - 1)) | ((hi & (T - 1)) << 16);
+    }
+}
+
+template <int BLOCK>
+__device__ __forceinline__ void p16_scan(const P16Ctx &pc) {
+    constexpr uint32_t T = Scan<BLOCK>::kT;
+    constexpr uint32_t HOT = (0xFFFFu & ~(T - 1)) * 0x00010001u;  // bits >= T in both halves
+    constexpr int NW4 = (1 << 15) / 4;  // 32768 words as uint4
+    const uint4 *h4 = reinterpret_cast<const uint4 *>(pc.h);
+    uint32_t hot = 0u;  // bit i: chunk threadIdx.x + i*BLOCK has a half >= T
+#pragma unroll
+    for (int i = 0; i < NW4 / BLOCK; ++i) {
+        const uint4 v = h4[threadIdx.x + i * BLOCK];
+        hot |= (uint32_t)(((v.x | v.y | v.z | v.w) & HOT) != 0u) << i;
+    }
+    if (hot) {
+        for (int i = 0; i < NW4 / BLOCK; ++i)
+            if ((hot >> i) & 1u) p16_scan_fix<T>(pc, (int)threadIdx.x + i * BLOCK);
+    }
+}
+
+// One wave counts the windows of tiles [t0, t1) that start in [ps, pe), over
+// `per` workgroup-uniform iterations (waves with fewer tiles idle through the
+// scan barriers).  Tiles are streamed two ahead; the decode of tile t+1 doubles as
+// lane 63's halo of tile t.
+template <int K, int R, int HM, int BLOCK>
+__device__ __forceinline__ void count_wave_range(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
+                                                 int64_t ps, int64_t pe, int64_t rl, int64_t rh, uint32_t *h,
+                                                 int lane, const P16Ctx &pc, uint32_t &nwin) {
+    constexpr int PF = KMC_PF;  // r[0] = tile t, r[i] = tile t+i
+    uint4 r[PF + 1];
+#pragma unroll
+    for (int q = 0; q <= PF; ++q) r[q] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t c_cur = 0u, v_cur = 0u;
+    P16Pending pd;
+    bool pending = false;
+    if (t0 < t1) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q)
+            if (t0 + q <= t1) r[q] = load_lane(data, t0 + q, lane, rl, rh);
+#if KMC_ABLATE == 2
+        c_cur = r[0].x ^ r[0].y;
+#else
+        decode16(r[0], c_cur, v_cur);
+#endif
+    }
+    for (int64_t i = 0; i < per; ++i) {
+        const int64_t t = t0 + i;
+        if (t < t1) {
+            r[PF] = make_uint4(0u, 0u, 0u, 0u);
+            if (t + PF <= t1) r[PF] = load_lane(data, t + PF, lane, rl, rh);
+            const uint4 r_cur = r[0], r_nxt = r[1];
+            uint32_t c_nxt, v_nxt;
+#if KMC_ABLATE == 2
+            c_nxt = r_nxt.x ^ r_nxt.y ^ r_nxt.z ^ r_nxt.w;
+            v_nxt = 0u;
+#else
+            decode16(r_nxt, c_nxt, v_nxt);
+#endif
+            // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
+            uint32_t hc = __shfl_down(c_cur, 1);
+            uint32_t hv = __shfl_down(v_cur, 1);
+            const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
+            const uint32_t v0 = __builtin_amdgcn_readlane(v_nxt, 0);
+            if (lane == 63) {
+                hc = c0;
+                hv = v0;
+            }
+            const int64_t base = t << kTileShift;
+            const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
+            if (interior && !__any((v_cur | hv) != 0u)) {
+                if constexpr (HM == 1) {
+                    if (pending) p16_check(pc, pd);
+                }
+                count_tile<K, R, HM, false>(c_cur, hc, 0xFFFFu, h, lane, pc, pd);
+                if constexpr (HM == 3) nwin += 16u;
+            } else {
+                // boundary tile or invalid bytes: exact per-window mask
+                const int64_t pos = base + (int64_t)lane * 16;
+                const int64_t dlo = ps - pos, dhi = pe - pos;
+                const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
+                const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
+                const uint32_t b_own = bad_mask16(r_cur);
+                uint32_t b_next = __shfl_down(b_own, 1);
+                const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
+                if (lane == 63) b_next = b0;
+                const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
+                if constexpr (HM == 1) {
+                    if (pending) p16_check(pc, pd);
+                }
+                count_tile<K, R, HM, true>(c_cur, hc, W, h, lane, pc, pd);
+                if constexpr (HM == 3) nwin += (uint32_t)__builtin_popcount(W);
+            }
+#pragma unroll
+            for (int q = 0; q < PF; ++q) r[q] = r[q + 1];
+            c_cur = c_nxt;
+            v_cur = v_nxt;
+            pending = (HM == 1);
+        }
+        if constexpr (HM == 1) {
+            if (pending && i + 1 == per) p16_check(pc, pd);
+        }
+        if constexpr (HM == 2) {
+            if ((i % Scan<BLOCK>::kTiles) == Scan<BLOCK>::kTiles - 1 && i + 1 < per) {
+                lds_barrier();
+                p16_scan<BLOCK>(pc);
+                lds_barrier();
+            }
+        }
+    }
+}
+
+template <int K, int R, int HM, class Idx, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
+    constexpr bool P16 = HM != 0;
+    static_assert(HM != 2 || (BLOCK / 64) * Scan<BLOCK>::kTiles * kTile + Scan<BLOCK>::kT <= 65536,
+                  "scan interval bound");
     constexpr int NB = 1 << (2 * K);
     constexpr int NW = P16 ? NB / 2 : NB * R;
     constexpr int NWAVES = BLOCK / 64;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t *h = smem;
-    uint32_t *misc = smem + NW;  // [0] spill count, [1],[2] first record (lo, hi)
+    uint32_t *misc = smem + NW;  // [0] spill count, [1],[2] first record, [3] windows added, [4] decoded sum
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar tile bookkeeping
     const int w = blockIdx.x;
     const Geom g = make_geom<Idx>(p);
     const int64_t tb = g.T0 + (int64_t)w * g.tpw;
     const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
     int64_t slot0 = -1, slot1 = -1;
+    uint64_t redo = 0, failed = 0;
+    if (p.fallback) {
+        redo = p.fail_mask[w];
+        if (redo == 0) return;  // nothing of this workgroup overflowed (uniform)
+    }
 
     if (tb < te) {
         const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
@@ -329,6 +574,8 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 }
             }
             misc[0] = 0u;
+            misc[3] = 0u;
+            misc[4] = 0u;
             misc[1] = (uint32_t)lo;
             misc[2] = (uint32_t)((uint64_t)lo >> 32);
         }
@@ -350,6 +597,13 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             const int64_t ps = ca > R0 ? ca : R0;
             const int64_t pe = ce < R1 ? ce : R1;
             if (ps >= pe) continue;
+            if (p.fallback) {  // recount only the flagged pieces (same piece numbering as the first pass)
+                const uint64_t bit = npieces < 63 ? (1ull << npieces) : (1ull << 63);
+                if ((redo & bit) == 0) {
+                    ++npieces;
+                    continue;
+                }
+            }
             pc.rec = s;
             // this piece's tiles, split into contiguous per-wave runs
             const int64_t tp0 = ps >> kTileShift;
@@ -357,7 +611,12 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
             const int64_t a0 = tp0 + (int64_t)wave * per;
             const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-            count_wave_range<K, R, P16>(p.data, a0, a1, ps, pe, g.rl, g.rh, h, lane, pc);
+            uint32_t nwin = 0u;
+            count_wave_range<K, R, HM, BLOCK>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, h, lane, pc, nwin);
+            if constexpr (HM == 3) {
+                const uint32_t wsum = wave_sum(nwin);
+                if (lane == 0) atomicAdd(&misc[3], wsum);
+            }
             __syncthreads();
             const bool entire = (ps == ca) && (pe == ce);
             int slot = 0;
@@ -368,9 +627,11 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             }
             uint32_t *dst = p.slab + ((int64_t)w * 2 + slot) * NB;
             if constexpr (P16) {
+                uint32_t dsum = 0u;
                 for (int i = tid; i < NW; i += BLOCK) {
                     const uint32_t v = h[i];
                     h[i] = 0u;
+                    dsum += (v & 0xFFFFu) + (v >> 16);
                     if (entire) {
                         p.sum[s + p.ld * (int64_t)i] = (int32_t)(v & 0xFFFFu);
                         p.sum[s + p.ld * (int64_t)(i + NW)] = (int32_t)(v >> 16);
@@ -378,6 +639,10 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                         dst[i] = v & 0xFFFFu;
                         dst[i + NW] = v >> 16;
                     }
+                }
+                if constexpr (HM == 3) {
+                    const uint32_t wsum = wave_sum(dsum);
+                    if (lane == 0) atomicAdd(&misc[4], wsum);
                 }
             } else {
                 for (int c = tid; c < NB; c += BLOCK) {
@@ -391,13 +656,26 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                     else dst[c] = v;
                 }
             }
-            ++npieces;
             __syncthreads();
+            if constexpr (HM == 3) {
+                // every 16-bit wrap only loses counts (low half: -65535 net, high half:
+                // -65536), so the decoded total equals the windows added iff none wrapped
+                if (tid == 0) {
+                    if (misc[3] != misc[4]) failed |= npieces < 63 ? (1ull << npieces) : (1ull << 63);
+                    misc[3] = 0u;
+                    misc[4] = 0u;
+                }
+                __syncthreads();
+            }
+            ++npieces;
         }
     }
     if (tid == 0) {
-        p.slot_rec[2 * w] = slot0;
-        p.slot_rec[2 * w + 1] = slot1;
+        if (!p.fallback) {
+            p.slot_rec[2 * w] = slot0;
+            p.slot_rec[2 * w + 1] = slot1;
+        }
+        if (HM == 3) p.fail_mask[w] = failed;
         if (p.spill_cnt) p.spill_cnt[w] = (tb < te) ? misc[0] : 0u;
     }
 }
@@ -469,14 +747,24 @@ __global__ __launch_bounds__(256) void invalid_kernel(Params p) {
 template <int K>
 struct Cfg;
 // R = replicas of each 32-bit bin; BLOCK = threads per workgroup
-template <> struct Cfg<1> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<2> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<3> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<4> { static constexpr int R = 32, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<5> { static constexpr int R = 8, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<6> { static constexpr int R = 2, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<7> { static constexpr int R = 1, BLOCK = 512; static constexpr bool P16 = false; };
-template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = 1024; static constexpr bool P16 = true; };
+// HM = histogram mode: 0 = 32-bit bins; k == 8 packed 16-bit halves with
+//   1 = returning adds + exact wrap fix-up, 2 = plain adds + overflow scans,
+//   3 = plain adds + wrap detection by total, pieces that wrapped recounted with 1.
+// KMC_K8_MODE selects the k == 8 mode (diagnostic builds compare them).
+#ifndef KMC_K8_MODE
+#define KMC_K8_MODE 3
+#endif
+template <> struct Cfg<1> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<2> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<3> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<4> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<5> { static constexpr int R = 8, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<6> { static constexpr int R = 2, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<7> { static constexpr int R = 1, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+#ifndef KMC_K8_BLOCK
+#define KMC_K8_BLOCK 1024
+#endif
+template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = KMC_K8_BLOCK, HM = KMC_K8_MODE; static constexpr bool P16 = true; };
 
 template <int K>
 constexpr size_t lds_bytes() {
@@ -496,7 +784,13 @@ thread_local hipEvent_t t_trace_after = nullptr;
 
 template <int K, class Idx>
 void *kernel_ptr() {
-    return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, Cfg<K>::P16, Idx, Cfg<K>::BLOCK>);
+    return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, Cfg<K>::HM, Idx, Cfg<K>::BLOCK>);
+}
+
+// The exact recount of pieces the optimistic k == 8 pass (HM 3) flagged.
+template <int K, class Idx>
+void *fallback_ptr() {
+    return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, 1, Idx, Cfg<K>::BLOCK>);
 }
 
 template <int K, class Idx>
@@ -515,6 +809,11 @@ int grid_size(int device, int &G) {
         const void *kp = kernel_ptr<K, Idx>();
         hipError_t e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<K>());
         if (e != hipSuccess) return (int)e;
+        if (Cfg<K>::HM == 3) {
+            e = hipFuncSetAttribute(fallback_ptr<K, Idx>(), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds_bytes<K>());
+            if (e != hipSuccess) return (int)e;
+        }
         int nb = 0;
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, Cfg<K>::BLOCK, lds_bytes<K>());
         if (e != hipSuccess) return (int)e;
@@ -527,7 +826,7 @@ int grid_size(int device, int &G) {
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct WsLayout {
-    size_t slot_rec, spill_cnt, slab, spill, total;
+    size_t slot_rec, spill_cnt, fail_mask, slab, spill, total;
 };
 
 inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
@@ -538,6 +837,8 @@ inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
     o += align256((size_t)G * 2 * sizeof(int64_t));
     L.spill_cnt = o;
     o += align256((size_t)G * sizeof(uint32_t));
+    L.fail_mask = o;
+    o += align256((size_t)G * sizeof(uint64_t));
     L.slab = o;
     o += align256((size_t)G * 2 * nb * sizeof(uint32_t));
     L.spill = o;
@@ -546,11 +847,12 @@ inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
     return L;
 }
 
-// Upper bound of the spill entries one workgroup can emit for `tiles` tiles:
-// each entry needs 65 536 increments of one 16-bit field (or pairs with one).
+// Upper bound of the spill entries one workgroup can emit for `tiles` tiles: a
+// scan entry (HM 2) stands for >= T >= 4096 increments of one 16-bit field; a wrap
+// entry (HM 1) for 65 536, or pairs with one.
 inline uint32_t spill_cap_for(int64_t tiles_per_wg) {
     const int64_t windows = tiles_per_wg * kTile;
-    return (uint32_t)(4 * (windows / 65536) + 64);
+    return (uint32_t)(windows / 4096 + 64);
 }
 
 struct Plan {
@@ -663,18 +965,30 @@ int run_dense(const Request &q, hipStream_t st) {
     p.slab = reinterpret_cast<uint32_t *>(base + pl.L.slab);
     p.spill = Cfg<K>::P16 ? reinterpret_cast<Spill *>(base + pl.L.spill) : nullptr;
     p.spill_cap = pl.spill_cap;
+    p.fail_mask = reinterpret_cast<uint64_t *>(base + pl.L.fail_mask);
+    p.fallback = 0;
 
     constexpr int NB = 1 << (2 * K);
     if (t_trace_before) {
         he = hipEventRecord(t_trace_before, st);
         if (he != hipSuccess) return (int)he;
     }
-    hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, Cfg<K>::P16, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
+    hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, Cfg<K>::HM, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
                        dim3(Cfg<K>::BLOCK), lds_bytes<K>(), st, p);
     he = hipGetLastError();
     if (he != hipSuccess) return (int)he;
     if (t_trace_after) {
         he = hipEventRecord(t_trace_after, st);
+        if (he != hipSuccess) return (int)he;
+    }
+    if (Cfg<K>::HM == 3) {
+        // exact recount of the pieces whose 16-bit counters wrapped (skewed input);
+        // workgroups with nothing flagged exit at once
+        Params pf = p;
+        pf.fallback = 1;
+        hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, 1, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
+                           dim3(Cfg<K>::BLOCK), lds_bytes<K>(), st, pf);
+        he = hipGetLastError();
         if (he != hipSuccess) return (int)he;
     }
     const int64_t cb = (NB + 255) / 256;

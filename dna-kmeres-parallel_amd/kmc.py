@@ -21,7 +21,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libkmc.so")
+LIB_PATH = os.environ.get("KMC_LIB") or os.path.join(HERE, "lib", "libkmc.so")
 HEADER = os.path.join(REPO, "include", "kmc.h")
 
 DIALECT_BLANK = 0  # importSeqs

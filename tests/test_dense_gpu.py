@@ -145,6 +145,29 @@ def test_k8_packed_counter_wraps(kmc, oracle, cuda):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
+def test_k8_overflow_fallback_mixed(kmc, oracle, cuda):
+    """Some workgroup pieces overflow their 16-bit counters (poly-A records, whole
+    or cut across workgroups), others do not: only those are recounted exactly."""
+    rng = np.random.default_rng(88)
+    lens, seqs = [], []
+    for i in range(60):
+        if i % 3 == 0:
+            seqs.append(np.full(70_000 + 37 * i, ord("A"), np.uint8))        # whole-record overflow
+        elif i % 3 == 1:
+            seqs.append(rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_000 + i))
+        else:
+            s = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=300_000)
+            s[50_000:250_000] = np.frombuffer(b"CCCCCCCT", np.uint8)[np.arange(200_000) % 8]
+            seqs.append(s)
+    recs = [np.append(s_, np.uint8(0)) for s_ in seqs]
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    got, inv = run_dense(kmc, cuda, data, idx, 8)
+    exp, exp_inv = oracle.count_dense(data, idx, 8)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
 @pytest.mark.parametrize("k", [4, 8])
 def test_range_shards_sum_to_full(kmc, oracle, cuda, k):
     """kmc_count_dense_ex over disjoint window ranges, each reading only its
