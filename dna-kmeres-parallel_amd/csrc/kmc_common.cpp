@@ -1,5 +1,5 @@
 // kmc_common.cpp — error strings and version of libkmc.so.
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 
 #include "kmc.h"
 

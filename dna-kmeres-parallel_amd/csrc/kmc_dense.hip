@@ -214,6 +214,14 @@ __device__ __forceinline__ uint32_t smear(uint32_t x) {
     return s;
 }
 
+// 1 or 0x10000 from bit `hb` (0/1): one v_mad_u32_u24 (hipcc otherwise emits
+// and + cmp + cndmask for the same select).
+__device__ __forceinline__ uint32_t half_inc(uint32_t hb) {
+    uint32_t r;
+    asm("v_mad_u32_u24 %0, %1, %2, 1" : "=v"(r) : "v"(hb), "s"(0xFFFFu));
+    return r;
+}
+
 // Per-piece context of the k == 8 packed-16-bit histogram.
 struct P16Ctx {
     uint32_t *h;
@@ -313,7 +321,7 @@ __device__ __forceinline__ void count_tile_p16(uint32_t lo, uint32_t hi, uint32_
         const uint32_t hb = (src >> (off + 15)) & 1u;
         pd.old[j] = 0u;
         if (!MASKED || ((W >> j) & 1u))
-            pd.old[j] = __hip_atomic_fetch_add(&pc.h[word], hb * 0xFFFFu + 1u, __ATOMIC_RELAXED,
+            pd.old[j] = __hip_atomic_fetch_add(&pc.h[word], half_inc(hb), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     pd.lo = lo;
@@ -364,7 +372,7 @@ __device__ __forceinline__ void count_tile_p16_plain(uint32_t lo, uint32_t hi, u
         const uint32_t word = (src >> off) & 0x7FFFu;
         const uint32_t hb = (src >> (off + 15)) & 1u;
         if (!MASKED || ((W >> j) & 1u))
-            __hip_atomic_fetch_add(&h[word], hb * 0xFFFFu + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&h[word], half_inc(hb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -387,6 +395,12 @@ __device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W,
     else
         count_tile32<K, R, MASKED>(lo, hi, W, h, lane);
 #endif
+}
+
+// Value of lane+1 (lane 63 gets 0): DPP wave_shl:1, no LDS traffic (unlike
+// __shfl_down, which is a ds_bpermute).
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
@@ -483,8 +497,8 @@ __device__ __forceinline__ void count_wave_range(const char *__restrict__ data, 
             decode16(r_nxt, c_nxt, v_nxt);
 #endif
             // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
-            uint32_t hc = __shfl_down(c_cur, 1);
-            uint32_t hv = __shfl_down(v_cur, 1);
+            uint32_t hc = from_next_lane(c_cur);
+            uint32_t hv = from_next_lane(v_cur);
             const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
             const uint32_t v0 = __builtin_amdgcn_readlane(v_nxt, 0);
             if (lane == 63) {
@@ -506,7 +520,7 @@ __device__ __forceinline__ void count_wave_range(const char *__restrict__ data, 
                 const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
                 const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
                 const uint32_t b_own = bad_mask16(r_cur);
-                uint32_t b_next = __shfl_down(b_own, 1);
+                uint32_t b_next = from_next_lane(b_own);
                 const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
                 if (lane == 63) b_next = b0;
                 const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
@@ -543,7 +557,9 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     constexpr int NB = 1 << (2 * K);
     constexpr int NW = P16 ? NB / 2 : NB * R;
     constexpr int NWAVES = BLOCK / 64;
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    // static LDS: the histogram's address is a link-time constant, folded into the
+    // ds_add offset (dynamic LDS costs one v_add per window)
+    __shared__ __attribute__((aligned(16))) uint32_t smem[NW + 8];
     uint32_t *h = smem;
     uint32_t *misc = smem + NW;  // [0] spill count, [1],[2] first record, [3] windows added, [4] decoded sum
 
@@ -758,18 +774,19 @@ template <> struct Cfg<1> { static constexpr int R = 32, BLOCK = 512, HM = 0; st
 template <> struct Cfg<2> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<3> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<4> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
-template <> struct Cfg<5> { static constexpr int R = 8, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
-template <> struct Cfg<6> { static constexpr int R = 2, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+#ifndef KMC_R5
+#define KMC_R5 8
+#endif
+#ifndef KMC_R6
+#define KMC_R6 2
+#endif
+template <> struct Cfg<5> { static constexpr int R = KMC_R5, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<6> { static constexpr int R = KMC_R6, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<7> { static constexpr int R = 1, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 #ifndef KMC_K8_BLOCK
 #define KMC_K8_BLOCK 1024
 #endif
 template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = KMC_K8_BLOCK, HM = KMC_K8_MODE; static constexpr bool P16 = true; };
-
-template <int K>
-constexpr size_t lds_bytes() {
-    return (Cfg<K>::P16 ? ((size_t)1 << (2 * K)) / 2 : ((size_t)1 << (2 * K)) * Cfg<K>::R) * 4 + 16;
-}
 
 struct DevInfo {
     int cus = 0;
@@ -787,11 +804,6 @@ void *kernel_ptr() {
     return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, Cfg<K>::HM, Idx, Cfg<K>::BLOCK>);
 }
 
-// The exact recount of pieces the optimistic k == 8 pass (HM 3) flagged.
-template <int K, class Idx>
-void *fallback_ptr() {
-    return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, 1, Idx, Cfg<K>::BLOCK>);
-}
 
 template <int K, class Idx>
 int grid_size(int device, int &G) {
@@ -807,15 +819,8 @@ int grid_size(int device, int &G) {
     const int ix = sizeof(Idx) == 8 ? 1 : 0;
     if (d.occ[K][ix] == 0) {
         const void *kp = kernel_ptr<K, Idx>();
-        hipError_t e = hipFuncSetAttribute(kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes<K>());
-        if (e != hipSuccess) return (int)e;
-        if (Cfg<K>::HM == 3) {
-            e = hipFuncSetAttribute(fallback_ptr<K, Idx>(), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds_bytes<K>());
-            if (e != hipSuccess) return (int)e;
-        }
-        int nb = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, Cfg<K>::BLOCK, lds_bytes<K>());
+        int nb = 0;  // the histogram is static LDS, accounted by the query itself
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kp, Cfg<K>::BLOCK, 0);
         if (e != hipSuccess) return (int)e;
         d.occ[K][ix] = nb > 0 ? nb : 1;
     }
@@ -974,20 +979,20 @@ int run_dense(const Request &q, hipStream_t st) {
         if (he != hipSuccess) return (int)he;
     }
     hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, Cfg<K>::HM, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
-                       dim3(Cfg<K>::BLOCK), lds_bytes<K>(), st, p);
+                       dim3(Cfg<K>::BLOCK), 0, st, p);
     he = hipGetLastError();
     if (he != hipSuccess) return (int)he;
     if (t_trace_after) {
         he = hipEventRecord(t_trace_after, st);
         if (he != hipSuccess) return (int)he;
     }
-    if (Cfg<K>::HM == 3) {
+    if constexpr (Cfg<K>::HM == 3) {
         // exact recount of the pieces whose 16-bit counters wrapped (skewed input);
         // workgroups with nothing flagged exit at once
         Params pf = p;
         pf.fallback = 1;
         hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, 1, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
-                           dim3(Cfg<K>::BLOCK), lds_bytes<K>(), st, pf);
+                           dim3(Cfg<K>::BLOCK), 0, st, pf);
         he = hipGetLastError();
         if (he != hipSuccess) return (int)he;
     }

@@ -71,6 +71,8 @@ def lib():
         L.kmc_count_dense_ex_workspace_size.restype = ctypes.c_size_t
         L.kmc_count_dense_ex_workspace_size.argtypes = [ctypes.POINTER(DenseArgs), ctypes.c_int]
         L.kmc_trace_set_events.argtypes = [_P, _P]
+        L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
+        L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.kmc_synth_fill.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
         L.kmc_synth_indices.argtypes = [_P, _U64, _U64]
         L.kmc_synth_indices.restype = None
@@ -200,6 +202,37 @@ def synth_indices(num_records, record_len):
     out = np.zeros(num_records + 1, dtype=np.int64)
     lib().kmc_synth_indices(out.ctypes.data_as(_P), num_records, record_len)
     return out
+
+
+# ---------------------------------------------------------------------------
+# sharding (host planning; device work in kmc_dist.py / kmc_count_multi)
+# ---------------------------------------------------------------------------
+class Shard(ctypes.Structure):
+    _fields_ = [("win_lo", _U64), ("win_hi", _U64), ("read_lo", _U64), ("read_hi", _U64)]
+
+
+def plan_shards(indices, k, nshards, align=4096):
+    """Byte-balanced shards of [indices[0], indices[-1]): list of (win_lo, win_hi, read_lo, read_hi)."""
+    idx = np.ascontiguousarray(indices, dtype=np.int64)
+    out = (Shard * nshards)()
+    _check(lib().kmc_plan_shards(idx.ctypes.data_as(_P), idx.size - 1, k, nshards, align, out), "kmc_plan_shards")
+    return [(s.win_lo, s.win_hi, s.read_lo, s.read_hi) for s in out]
+
+
+def count_multi(data, indices, k, ndev=1, devices=None, invalid=False):
+    """Single-process multi-GPU count of a host buffer (kmc_count_multi: shards + RCCL all-reduce)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    idx = np.ascontiguousarray(indices, dtype=np.int64)
+    n = idx.size - 1
+    out = np.zeros((1 << (2 * k), n), dtype=np.int32)
+    inv = np.zeros(n, dtype=np.int32) if invalid else None
+    devs = None
+    if devices is not None:
+        devs = (ctypes.c_int * ndev)(*devices)
+    rc = lib().kmc_count_multi(data.ctypes.data_as(_P), idx.ctypes.data_as(_P), n, data.size, k, ndev, devs,
+                               out.ctypes.data_as(_P), inv.ctypes.data_as(_P) if inv is not None else None)
+    _check(rc, "kmc_count_multi")
+    return out, inv
 
 
 # ---------------------------------------------------------------------------

@@ -119,6 +119,29 @@ size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *args, int device)
 int kmc_count_dense_ex(const kmc_dense_args *args, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* Sharding.  A shard counts the windows starting in
+ * [win_lo, win_hi) and reads data[read_lo, read_hi) = its bytes plus a k-1 byte
+ * halo.  kmc_plan_shards cuts the buffer [indices[0], indices[num_seqs]) into
+ * nshards contiguous, byte-balanced ranges whose inner cut points are multiples
+ * of `align` (0 -> 4096); a shard may be empty.  Host memory, no device needed. */
+typedef struct kmc_shard {
+    uint64_t win_lo, win_hi;
+    uint64_t read_lo, read_hi;
+} kmc_shard;
+
+int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, int nshards, uint64_t align,
+                    kmc_shard *out);
+
+/* Single-process multi-GPU count of a host buffer (the C++ host driver's path):
+ * shards the buffer over `ndev` devices (kmc_plan_shards), copies each shard +
+ * halo to its device, counts it there (kmc_count_dense_ex) and sums the per-device
+ * matrices with one RCCL all-reduce (int32, sum) over xGMI; the result
+ * sum[s + num_seqs*code] (and optional invalid[s]) is copied back to host
+ * memory.  devices == NULL -> 0 .. ndev-1.  Synchronous. */
+int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes, int k,
+                    int ndev, const int *devices, int32_t *sum, int32_t *invalid);
+
+/* ------------------------------------------------------------------------ */
 /* Tracing (the reference times step 1 with cudaEvents, main.cu:262-300): when set,
  * every following dense count call on this host thread records `before` right
  * before its histogram kernel and `after` right after it, on the call's stream,

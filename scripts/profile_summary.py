@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Turn gpurun_out/prof_bench/ (scripts/profile_bench.sh) into committed profiles/:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary of the bench command
+  profiles/<tag>_bench_trace.json   the bench JSON line printed under the profiler
+  profiles/pmc_dense_k8_10gbase.json  HBM bytes per histogram launch (bench.py reads it)
+FETCH_SIZE is counted in KiB and, on gfx950, reads half the bytes of a wide
+streaming read (MI355X_MICROARCH.md §HBM): bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(REPO, "gpurun_out", "prof_bench")
+DST = os.path.join(REPO, "profiles")
+
+
+def per_launch(counter_dir, counter, name_sub):
+    vals = []
+    for f in glob.glob(os.path.join(counter_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == counter and name_sub in row["Kernel_Name"]:
+                    vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    os.makedirs(DST, exist_ok=True)
+    stats = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(DST, "%s_kernel_stats.csv" % tag))
+    line = None
+    with open(os.path.join(SRC, "trace.log")) as fh:
+        for l in fh:
+            if l.startswith("{"):
+                line = json.loads(l)
+    if line:
+        with open(os.path.join(DST, "%s_bench_trace.json" % tag), "w") as fh:
+            json.dump(line, fh, indent=1)
+    k = line["config"]["k"] if line else 8
+    kern = "count_dense_kernel<%d," % k
+    fetch = per_launch(os.path.join(SRC, "fetch"), "FETCH_SIZE", kern)
+    write = per_launch(os.path.join(SRC, "write"), "WRITE_SIZE", kern)
+    if fetch and write and line:
+        f = sum(fetch) / len(fetch)
+        w = sum(write) / len(write)
+        out = {
+            "k": k,
+            "data_bytes": line["config"]["records_per_gpu"] * (line["config"]["record_len"] + 1),
+            "kernel": kern,
+            "fetch_size_kib_per_launch": f,
+            "write_size_kib_per_launch": w,
+            "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+            "correction": "gfx950: FETCH_SIZE x2 for 16-B/lane streaming reads (MI355X_MICROARCH.md HBM section)",
+            "launches_sampled": [len(fetch), len(write)],
+            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of python3 bench.py --steps 3",
+        }
+        with open(os.path.join(DST, "pmc_dense_k8_10gbase.json"), "w") as fh:
+            json.dump(out, fh, indent=1)
+        print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -242,3 +242,28 @@ def test_synthetic_1gbase_k8_full_parity(kmc, oracle, cuda):
     np.testing.assert_array_equal(got, exp)
     assert (inv.cpu().numpy() == 0).all() and (exp_inv == 0).all()
     assert int(got.astype(np.int64).sum()) == nrec * (L - 8 + 1)
+
+
+@pytest.mark.parametrize("nshards", [2, 7])
+def test_gpu_counter_over_planned_shards(kmc, oracle, cuda, nshards):
+    """kmc_dist.gpu_counter on each planned shard (only shard + halo on the device)
+    sums to the full histogram: the per-rank work of the N-GPU path."""
+    import kmc_dist
+    rng = np.random.default_rng(21)
+    data, idx = random_records(rng, [300_000, 5, 123_457, 64_000], 0.002, 0.002)
+    exp, _ = oracle.count_dense(data, idx, 8)
+    count = kmc_dist.gpu_counter(cuda)
+    acc = np.zeros_like(exp)
+    for shard in kmc.plan_shards(idx, 8, nshards):
+        acc += count(data, idx, 8, shard).cpu().numpy()
+    np.testing.assert_array_equal(acc, exp)
+
+
+def test_count_multi_single_device(kmc, oracle, cuda):
+    """kmc_count_multi (host buffer -> shards -> RCCL all-reduce) on the box's one GPU."""
+    rng = np.random.default_rng(22)
+    data, idx = random_records(rng, [200_000, 77_777, 3], 0.003, 0.003)
+    got, inv = kmc.count_multi(data, idx, 5, ndev=1, invalid=True)
+    exp, exp_inv = oracle.count_dense(data, idx, 5)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
