@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--records", type=int, default=10, help="records per GPU")
     ap.add_argument("--record-len", type=int, default=1_000_000_000, help="bases per record")
-    ap.add_argument("--cpu-sample", type=int, default=24_000_000,
+    ap.add_argument("--cpu-sample", type=int, default=64_000_000,
                     help="bases per CPU thread for the reference CPU baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_dense_k8_10gbase.json"),
