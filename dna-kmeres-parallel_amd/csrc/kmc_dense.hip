@@ -33,27 +33,10 @@
 
 #include "kmc.h"
 #include "kmc_internal.h"
-
-// Diagnostic builds only (scripts/kbench.py): KMC_ABLATE=1 replaces the LDS
-// histogram update by a register XOR (codes still computed), KMC_ABLATE=2 also
-// skips the decode (loads only).  The shipped library is built with KMC_ABLATE=0.
-#ifndef KMC_ABLATE
-#define KMC_ABLATE 0
-#endif
-// Tiles kept in flight per wave ahead of the one being counted, and whether the
-// once-read sequence stream uses non-temporal (nt) loads.
-#ifndef KMC_PF
-#define KMC_PF 2
-#endif
-#ifndef KMC_NT
-#define KMC_NT 0
-#endif
+#include "kmc_stream.h"
 
 namespace kmc {
 namespace {
-
-constexpr int kTileShift = 10;  // 1 KiB per wave per tile
-constexpr int kTile = 1 << kTileShift;
 
 struct Spill {
     int64_t rec;
@@ -79,140 +62,6 @@ struct Params {
     uint64_t *fail_mask;     // [G] HM 3: bit i = i-th piece of the workgroup overflowed (bit 63: any >= 63)
     int fallback;            // 1: recount only the pieces flagged in fail_mask (exact HM 1 kernel)
 };
-
-struct Geom {
-    int64_t wl, wh, rl, rh;
-    int64_t T0, T1, tpw;
-};
-
-template <class Idx>
-__device__ __forceinline__ int64_t rec_off(const Params &p, int64_t i) {
-    return (int64_t)((const Idx *)p.indices)[i];
-}
-
-template <class Idx>
-__device__ __forceinline__ Geom make_geom(const Params &p) {
-    Geom g;
-    if (p.derive) {
-        g.wl = rec_off<Idx>(p, 0);
-        g.wh = rec_off<Idx>(p, p.n);
-        g.rl = g.wl;
-        g.rh = g.wh;
-    } else {
-        g.wl = p.wl;
-        g.wh = p.wh;
-        g.rl = p.rl;
-        g.rh = p.rh;
-    }
-    if (g.wh <= g.wl) {
-        g.T0 = g.T1 = 0;
-        g.tpw = 1;
-    } else {
-        g.T0 = g.wl >> kTileShift;
-        g.T1 = (g.wh + kTile - 1) >> kTileShift;
-        g.tpw = (g.T1 - g.T0 + p.G - 1) / p.G;
-    }
-    return g;
-}
-
-// Window range of record s clipped to the counted range: [ca, ce).
-template <int K, class Idx>
-__device__ __forceinline__ void record_windows(const Params &p, const Geom &g, int64_t s, int64_t &ca,
-                                               int64_t &ce) {
-    const int64_t a = rec_off<Idx>(p, s);
-    const int64_t e = rec_off<Idx>(p, s + 1);
-    const int64_t nw = e - a - K > 0 ? e - a - K : 0;  // kernels.h:133 generalised
-    ca = a > g.wl ? a : g.wl;
-    ce = (a + nw) < g.wh ? (a + nw) : g.wh;
-}
-
-// ---------------------------------------------------------------------------
-// decode: 16 ASCII bytes (one lane's chunk) -> 32-bit word of 2-bit codes, base i
-// at bits 2i (the reference's little-endian bin order), plus validity.
-//
-// The low 3 bits of A,C,G,T are 1,3,7,4 and distinct, so one v_perm_b32 on
-// (w & 0x07070707) maps every byte to its code (a 4-entry table lookup per
-// byte) and a second one to the letter that code stands for; a byte is valid
-// iff it equals that letter (lowercase, N, '\r', '\0', ... never do).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kCodeLo = 0x01000000u;   // table[0..3] = {-, A=0, -, C=1}
-constexpr uint32_t kCodeHi = 0x02000003u;   // table[4..7] = {T=3, -, -, G=2}
-constexpr uint32_t kCanonLo = 0x43FF41FFu;  // table[0..3] = {xx, 'A', xx, 'C'}
-constexpr uint32_t kCanonHi = 0x47FFFF54u;  // table[4..7] = {'T', xx, xx, 'G'}
-
-__device__ __forceinline__ uint32_t byte_codes(uint32_t w) {
-    return __builtin_amdgcn_perm(kCodeHi, kCodeLo, w & 0x07070707u);
-}
-__device__ __forceinline__ uint32_t byte_mismatch(uint32_t w) {  // 0 in every valid byte
-    return w ^ __builtin_amdgcn_perm(kCanonHi, kCanonLo, w & 0x07070707u);
-}
-
-// code = 16 packed 2-bit codes; bad = OR of the per-byte mismatches (0 iff all valid)
-__device__ __forceinline__ void decode16(const uint4 r, uint32_t &code, uint32_t &bad) {
-    const uint32_t c0 = byte_codes(r.x), c1 = byte_codes(r.y), c2 = byte_codes(r.z), c3 = byte_codes(r.w);
-    bad = byte_mismatch(r.x) | byte_mismatch(r.y) | byte_mismatch(r.z) | byte_mismatch(r.w);
-    // bytes -> nibbles -> one byte per dword (base 4d+i at bits 2(4d+i))
-    const uint32_t u = __builtin_amdgcn_perm(c1, c0, 0x06040200u) | (__builtin_amdgcn_perm(c1, c0, 0x07050301u) << 2);
-    const uint32_t v = __builtin_amdgcn_perm(c3, c2, 0x06040200u) | (__builtin_amdgcn_perm(c3, c2, 0x07050301u) << 2);
-    code = __builtin_amdgcn_perm(v, u, 0x06040200u) | (__builtin_amdgcn_perm(v, u, 0x07050301u) << 4);
-}
-
-// 16-bit invalid-base mask of a chunk (slow path only)
-__device__ __forceinline__ uint32_t bad_mask16(const uint4 r) {
-    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-    uint32_t bad = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        const uint32_t x = byte_mismatch(w[d]);
-        const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-        bad |= ((((nz >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * d);
-    }
-    return bad;
-}
-
-// One lane's 16 bytes of tile t; bytes outside [rl, rh) read as 0 (invalid).
-__device__ __forceinline__ uint4 load_lane(const char *__restrict__ data, int64_t t, int lane, int64_t rl,
-                                           int64_t rh) {
-    const int64_t base = t << kTileShift;
-    const int64_t q = base + (int64_t)lane * 16;
-    if (base >= rl && base + kTile <= rh) {  // wave-uniform: whole tile readable
-#if KMC_NT
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(data + q));
-        return make_uint4(x[0], x[1], x[2], x[3]);
-#else
-        return *reinterpret_cast<const uint4 *>(data + q);
-#endif
-    }
-    uint32_t v[4] = {0u, 0u, 0u, 0u};
-    if (q >= rl && q + 16 <= rh) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(data + q);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-    } else {
-#pragma unroll 1
-        for (int i = 0; i < 16; ++i) {
-            const int64_t b = q + i;
-            if (b >= rl && b < rh) v[i >> 2] |= (uint32_t)(uint8_t)data[b] << (8 * (i & 3));
-        }
-    }
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-
-// OR of x >> 0 .. x >> (K-1): bit j set iff any of bases j .. j+K-1 is invalid.
-template <int K>
-__device__ __forceinline__ uint32_t smear(uint32_t x) {
-    uint32_t s = x;
-    int c = 1;
-#pragma unroll
-    for (int it = 0; it < 6; ++it) {
-        if (c < K) {
-            const int st = (c < K - c) ? c : (K - c);
-            s |= s >> st;
-            c += st;
-        }
-    }
-    return s;
-}
 
 // 1 or 0x10000 from bit `hb` (0/1): one v_mad_u32_u24 (hipcc otherwise emits
 // and + cmp + cndmask for the same select).
@@ -379,42 +228,12 @@ __device__ __forceinline__ void count_tile_p16_plain(uint32_t lo, uint32_t hi, u
 template <int K, int R, int HM, bool MASKED>
 __device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h, int lane,
                                            const P16Ctx &pc, P16Pending &pd) {
-#if KMC_ABLATE == 1
-    const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);
-    uint32_t x = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) x ^= (j <= 16 - K) ? (lo >> (2 * j)) : (mid >> (2 * (j - 8)));
-    asm volatile("" ::"v"(x), "v"(W));
-#elif KMC_ABLATE == 2
-    asm volatile("" ::"v"(lo), "v"(hi), "v"(W));
-#else
     if constexpr (HM == 1)
         count_tile_p16<MASKED>(lo, hi, W, pc, pd);
     else if constexpr (HM == 2 || HM == 3)
         count_tile_p16_plain<MASKED>(lo, hi, W, h);
     else
         count_tile32<K, R, MASKED>(lo, hi, W, h, lane);
-#endif
-}
-
-// Value of lane+1 (lane 63 gets 0): DPP wave_shl:1, no LDS traffic (unlike
-// __shfl_down, which is a ds_bpermute).
-__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    return x;
-}
-
-// Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for
-// the wave's outstanding global loads, so the tile prefetch keeps streaming.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // HM == 2 overflow scans.  Between two scans the workgroup adds at most
@@ -458,84 +277,30 @@ __device__ __forceinline__ void p16_scan(const P16Ctx &pc) {
     }
 }
 
-// One wave counts the windows of tiles [t0, t1) that start in [ps, pe), over
-// `per` workgroup-uniform iterations (waves with fewer tiles idle through the
-// scan barriers).  Tiles are streamed two ahead; the decode of tile t+1 doubles as
-// lane 63's halo of tile t.
+// The dense histogram as a stream_tiles operation (one per histogram mode).
 template <int K, int R, int HM, int BLOCK>
-__device__ __forceinline__ void count_wave_range(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
-                                                 int64_t ps, int64_t pe, int64_t rl, int64_t rh, uint32_t *h,
-                                                 int lane, const P16Ctx &pc, uint32_t &nwin) {
-    constexpr int PF = KMC_PF;  // r[0] = tile t, r[i] = tile t+i
-    uint4 r[PF + 1];
-#pragma unroll
-    for (int q = 0; q <= PF; ++q) r[q] = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t c_cur = 0u, v_cur = 0u;
+struct DenseOp {
+    uint32_t *h;
+    int lane;
+    const P16Ctx &pc;
     P16Pending pd;
     bool pending = false;
-    if (t0 < t1) {
-#pragma unroll
-        for (int q = 0; q < PF; ++q)
-            if (t0 + q <= t1) r[q] = load_lane(data, t0 + q, lane, rl, rh);
-#if KMC_ABLATE == 2
-        c_cur = r[0].x ^ r[0].y;
-#else
-        decode16(r[0], c_cur, v_cur);
-#endif
-    }
-    for (int64_t i = 0; i < per; ++i) {
-        const int64_t t = t0 + i;
-        if (t < t1) {
-            r[PF] = make_uint4(0u, 0u, 0u, 0u);
-            if (t + PF <= t1) r[PF] = load_lane(data, t + PF, lane, rl, rh);
-            const uint4 r_cur = r[0], r_nxt = r[1];
-            uint32_t c_nxt, v_nxt;
-#if KMC_ABLATE == 2
-            c_nxt = r_nxt.x ^ r_nxt.y ^ r_nxt.z ^ r_nxt.w;
-            v_nxt = 0u;
-#else
-            decode16(r_nxt, c_nxt, v_nxt);
-#endif
-            // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
-            uint32_t hc = from_next_lane(c_cur);
-            uint32_t hv = from_next_lane(v_cur);
-            const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
-            const uint32_t v0 = __builtin_amdgcn_readlane(v_nxt, 0);
-            if (lane == 63) {
-                hc = c0;
-                hv = v0;
-            }
-            const int64_t base = t << kTileShift;
-            const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
-            if (interior && !__any((v_cur | hv) != 0u)) {
-                if constexpr (HM == 1) {
-                    if (pending) p16_check(pc, pd);
-                }
-                count_tile<K, R, HM, false>(c_cur, hc, 0xFFFFu, h, lane, pc, pd);
-                if constexpr (HM == 3) nwin += 16u;
-            } else {
-                // boundary tile or invalid bytes: exact per-window mask
-                const int64_t pos = base + (int64_t)lane * 16;
-                const int64_t dlo = ps - pos, dhi = pe - pos;
-                const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
-                const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
-                const uint32_t b_own = bad_mask16(r_cur);
-                uint32_t b_next = from_next_lane(b_own);
-                const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
-                if (lane == 63) b_next = b0;
-                const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
-                if constexpr (HM == 1) {
-                    if (pending) p16_check(pc, pd);
-                }
-                count_tile<K, R, HM, true>(c_cur, hc, W, h, lane, pc, pd);
-                if constexpr (HM == 3) nwin += (uint32_t)__builtin_popcount(W);
-            }
-#pragma unroll
-            for (int q = 0; q < PF; ++q) r[q] = r[q + 1];
-            c_cur = c_nxt;
-            v_cur = v_nxt;
-            pending = (HM == 1);
+    uint32_t nwin = 0u;  // HM 3: windows this lane added
+
+    __device__ DenseOp(uint32_t *h_, int lane_, const P16Ctx &pc_) : h(h_), lane(lane_), pc(pc_) {}
+
+    __device__ __forceinline__ void before_tile() {
+        if constexpr (HM == 1) {
+            if (pending) p16_check(pc, pd);
         }
+    }
+    template <bool MASKED>
+    __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
+        count_tile<K, R, HM, MASKED>(lo, hi, W, h, lane, pc, pd);
+        if constexpr (HM == 1) pending = true;
+        if constexpr (HM == 3) nwin += MASKED ? (uint32_t)__builtin_popcount(W) : 16u;
+    }
+    __device__ __forceinline__ void after_iter(int64_t i, int64_t per, bool) {
         if constexpr (HM == 1) {
             if (pending && i + 1 == per) p16_check(pc, pd);
         }
@@ -547,7 +312,7 @@ __device__ __forceinline__ void count_wave_range(const char *__restrict__ data, 
             }
         }
     }
-}
+};
 
 template <int K, int R, int HM, class Idx, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
@@ -627,10 +392,10 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
             const int64_t a0 = tp0 + (int64_t)wave * per;
             const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-            uint32_t nwin = 0u;
-            count_wave_range<K, R, HM, BLOCK>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, h, lane, pc, nwin);
+            DenseOp<K, R, HM, BLOCK> op(h, lane, pc);
+            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
             if constexpr (HM == 3) {
-                const uint32_t wsum = wave_sum(nwin);
+                const uint32_t wsum = wave_sum(op.nwin);
                 if (lane == 0) atomicAdd(&misc[3], wsum);
             }
             __syncthreads();
@@ -1074,6 +839,10 @@ extern "C" int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, un
 
 extern "C" size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *a, int device) {
     if (!a || a->k < 1 || a->k > KMC_DENSE_MAX_K) return 0;
+    if (a->k > 8) {
+        size_t sz = 0;
+        return radix_dense(a, nullptr, true, &sz) == 0 ? sz : 0;
+    }
     const int64_t wl = (int64_t)a->win_lo, wh = (int64_t)a->win_hi;
     return workspace_for<int64_t>(a->k, device, false, wl, wh);
 }
@@ -1086,6 +855,7 @@ extern "C" int kmc_count_dense_ex(const kmc_dense_args *a, hipStream_t stream) {
     if (reinterpret_cast<uintptr_t>(a->data) & 15u) return KMC_ERR_ALIGNMENT;
     if (a->read_hi < a->read_lo || a->win_hi < a->win_lo) return KMC_ERR_INVALID_ARG;
     if (a->sum_ld != 0 && a->sum_ld < a->num_seqs) return KMC_ERR_INVALID_ARG;
+    if (a->k > 8) return radix_dense(a, stream, false, nullptr);
     Request q{};
     q.data = a->data;
     q.indices = a->indices;
@@ -1104,8 +874,15 @@ extern "C" int kmc_count_dense_ex(const kmc_dense_args *a, hipStream_t stream) {
 }
 
 extern "C" size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device) {
-    (void)num_seqs;
     if (k < 1 || k > KMC_DENSE_MAX_K) return 0;
+    if (k > 8) {
+        kmc_dense_args a{};
+        a.k = k;
+        a.num_seqs = num_seqs;
+        a.read_hi = a.win_hi = data_bytes;
+        size_t sz = 0;
+        return radix_dense(&a, nullptr, true, &sz) == 0 ? sz : 0;
+    }
     return workspace_for<int64_t>(k, device, false, 0, (int64_t)data_bytes);
 }
 

@@ -2,7 +2,14 @@
 #pragma once
 #include <cstdint>
 
+struct kmc_dense_args;
+typedef struct ihipStream_t *hipStream_t;
+
 namespace kmc {
+// 9 <= k <= KMC_DENSE_MAX_K: radix-partitioned dense counting (kmc_radix.hip).
+// size_only: report the workspace size in *size_out instead of launching.
+int radix_dense(const ::kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out);
+
 // splitmix64 output n (0-based) of the stream seeded with `seed` (Steele et al.):
 // z = seed + (n+1)*golden; two xor-shift-multiply rounds; final xor-shift.
 __host__ __device__ inline uint64_t splitmix64_at(uint64_t seed, uint64_t n) {

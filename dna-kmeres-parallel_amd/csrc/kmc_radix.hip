@@ -1,0 +1,428 @@
+// kmc_radix.hip — dense k-mer histograms for 9 <= k <= KMC_DENSE_MAX_K (BASELINE
+// config C3: k = 13, 67 M bins per record), whose 4^k bins cannot be privatised
+// in LDS.  Same counting contract and output layout as kmc_dense.hip (the
+// generalisation of permutationsCountAll, main.cu:636-646, in the GPU layout of
+// kernels.h:142), computed by a two-level radix partition:
+//
+//   R1 count    every workgroup streams its tiles (kmc_stream.h) and counts, per
+//               record piece, the windows of each bucket b = code >> 15 in LDS
+//               -> cnt[(s*NBK + b)*G + w]
+//   R2 scan     exclusive prefix sum -> 64-bit offsets: list (s, b) is contiguous,
+//               workgroup segments inside it in w order
+//   R3 scatter  the same traversal writes each window's low 15 code bits
+//               (uint16) at its list position (LDS 64-bit cursors per bucket)
+//   R4 hist     one workgroup per list: 32 768-bin LDS histogram of its entries ->
+//               stage[s][b*32768 + c] (record-major, coalesced)
+//   R5 place    transpose stage into sum[s + ld*code] (k-mer-major, coalesced)
+//
+// Bytes per k-mer: 1 (R1) + 1 (R3) input, 2 written + 2 read entries, plus the
+// output twice; the LDS histograms see the same bank-conflict-bound atomic rate
+// as the k <= 8 kernels.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "kmc.h"
+#include "kmc_internal.h"
+#include "kmc_stream.h"
+
+namespace kmc {
+namespace {
+
+constexpr int kLowBits = 15;  // bins per bucket: 2^15 x 32-bit = 128 KB of LDS
+constexpr int kBucketBins = 1 << kLowBits;
+
+struct RParams {
+    const char *data;
+    const void *indices;
+    int64_t n;
+    int64_t wl, wh, rl, rh;
+    int derive;
+    int G;           // workgroups of R1/R3
+    int nbk;         // buckets per record
+    uint32_t *cnt;   // [n][nbk][G]
+    uint64_t *off;   // [n*nbk*G + 1] exclusive prefix of cnt
+    uint16_t *ent;   // entries
+    uint32_t *stage; // [n][4^k]
+    int32_t *sum;
+    int64_t ld;
+    int32_t *invalid;
+};
+
+template <int K>
+struct RCountOp {
+    uint32_t *c;  // LDS bucket counters
+    __device__ void before_tile() {}
+    template <bool MASKED>
+    __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t code = window_code_rt<K>(lo, hi, j);
+            if (!MASKED || ((W >> j) & 1u))
+                __hip_atomic_fetch_add(&c[code >> kLowBits], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    __device__ void after_iter(int64_t, int64_t, bool) {}
+};
+
+template <int K>
+struct RScatterOp {
+    unsigned long long *cur;  // LDS cursors: global position of the next entry per bucket
+    uint16_t *ent;
+    __device__ void before_tile() {}
+    template <bool MASKED>
+    __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t code = window_code_rt<K>(lo, hi, j);
+            if (!MASKED || ((W >> j) & 1u)) {
+                const unsigned long long pos = __hip_atomic_fetch_add(
+                    &cur[code >> kLowBits], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ent[pos] = (uint16_t)(code & (kBucketBins - 1));
+            }
+        }
+    }
+    __device__ void after_iter(int64_t, int64_t, bool) {}
+};
+
+// R1 and R3: the piece walk of the dense kernel; SCATTER selects the op.
+template <int K, class Idx, bool SCATTER, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
+    constexpr int NWAVES = BLOCK / 64;
+    constexpr int NBK = 1 << (2 * K - kLowBits);
+    __shared__ __attribute__((aligned(16))) unsigned long long lds64[NBK];
+    __shared__ int64_t s_first;
+    uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds64);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = blockIdx.x;
+    const Geom g = make_geom<Idx>(p);
+    const int64_t tb = g.T0 + (int64_t)w * g.tpw;
+    const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
+    if (tb >= te) return;
+    const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
+    const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
+    if (tid == 0) s_first = first_record_at<Idx>(p, R0);
+    __syncthreads();
+    for (int64_t s = s_first; s < p.n; ++s) {
+        if (rec_off<Idx>(p, s) >= R1) break;
+        int64_t ca, ce;
+        record_windows<K, Idx>(p, g, s, ca, ce);
+        const int64_t ps = ca > R0 ? ca : R0;
+        const int64_t pe = ce < R1 ? ce : R1;
+        if (ps >= pe) continue;
+        const int64_t lbase = (s * NBK) * p.G + w;  // cnt/off index of (s, b=0, w); stride G per bucket
+        for (int b = tid; b < NBK; b += BLOCK) {
+            if (SCATTER) lds64[b] = p.off[lbase + (int64_t)b * p.G];
+            else lds32[b] = 0u;
+        }
+        __syncthreads();
+        const int64_t tp0 = ps >> kTileShift;
+        const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
+        const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
+        const int64_t a0 = tp0 + (int64_t)wave * per;
+        const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
+        if constexpr (SCATTER) {
+            RScatterOp<K> op{lds64, p.ent};
+            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        } else {
+            RCountOp<K> op{lds32};
+            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        }
+        __syncthreads();
+        if constexpr (!SCATTER) {
+            for (int b = tid; b < NBK; b += BLOCK) p.cnt[lbase + (int64_t)b * p.G] = lds32[b];
+        }
+        __syncthreads();
+    }
+}
+
+// R2: exclusive scan of cnt (uint32) into off (uint64), three phases.
+constexpr int kScanBlock = 1024, kScanPer = 4, kScanTile = kScanBlock * kScanPer;
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint64_t t = lane < kScanBlock / 64 ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(t, o);
+            if (lane >= o) t += y;
+        }
+        if (lane < kScanBlock / 64) sh[lane] = t;
+    }
+    __syncthreads();
+    total = sh[kScanBlock / 64 - 1];
+    const uint64_t before = wid ? sh[wid - 1] : 0;
+    __syncthreads();
+    return before + x - v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t *in, int64_t m, uint64_t *bsum) {
+    __shared__ uint64_t sh[kScanBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    uint64_t v = 0;
+    for (int q = 0; q < kScanPer; ++q) {
+        const int64_t i = base + (int64_t)q * kScanBlock + threadIdx.x;
+        if (i < m) v += in[i];
+    }
+    uint64_t total;
+    block_excl_scan(v, sh, total);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_blocks_kernel(uint64_t *bsum, int64_t nb) {
+    __shared__ uint64_t sh[kScanBlock / 64];
+    uint64_t carry = 0;
+    for (int64_t base = 0; base < nb; base += kScanBlock) {
+        const int64_t i = base + threadIdx.x;
+        const uint64_t v = i < nb ? bsum[i] : 0;
+        uint64_t total;
+        const uint64_t ex = block_excl_scan(v, sh, total);
+        if (i < nb) bsum[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t *in, int64_t m, const uint64_t *bsum,
+                                                                uint64_t *out) {
+    __shared__ uint64_t sh[kScanBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+    uint64_t v[kScanPer], tsum = 0;
+    for (int q = 0; q < kScanPer; ++q) {
+        v[q] = (base + q < m) ? in[base + q] : 0;
+        tsum += v[q];
+    }
+    uint64_t total;
+    uint64_t run = bsum[blockIdx.x] + block_excl_scan(tsum, sh, total);
+    for (int q = 0; q < kScanPer; ++q) {
+        if (base + q < m) out[base + q] = run;
+        run += v[q];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) out[m] = run;  // grand total
+}
+
+// R4: one workgroup per list (s, b).
+__global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbins) {
+    __shared__ __attribute__((aligned(16))) uint32_t h[kBucketBins];
+    const int64_t list = blockIdx.x;  // s*nbk + b
+    const int64_t s = list / p.nbk, b = list % p.nbk;
+    for (int i = threadIdx.x; i < kBucketBins; i += 1024) h[i] = 0u;
+    __syncthreads();
+    const uint64_t beg = p.off[list * p.G], end = p.off[(list + 1) * p.G];
+    // head up to 8-entry alignment, 16-B vector body, tail
+    uint64_t a = beg;
+    const uint64_t abody = (beg + 7) & ~(uint64_t)7;
+    if (a + threadIdx.x < (abody < end ? abody : end))
+        atomicAdd(&h[p.ent[a + threadIdx.x]], 1u);
+    a = abody;
+    if (a < end) {
+        const uint64_t nvec = (end - a) / 8;
+        const uint4 *v = reinterpret_cast<const uint4 *>(p.ent + a);
+        for (uint64_t i = threadIdx.x; i < nvec; i += 1024) {
+            const uint4 x = v[i];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __hip_atomic_fetch_add(&h[w[q] & 0xFFFFu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&h[w[q] >> 16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        const uint64_t t = a + nvec * 8;
+        if (t + threadIdx.x < end) atomicAdd(&h[p.ent[t + threadIdx.x]], 1u);
+    }
+    __syncthreads();
+    uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
+    for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
+}
+
+// R5: stage [n][nbins] -> sum[s + ld*code]; one workgroup per 256 codes.
+__global__ __launch_bounds__(256) void radix_place_kernel(RParams p, int64_t nbins) {
+    const int64_t c0 = (int64_t)blockIdx.x * 256;
+    const int64_t total = 256 * p.n;  // outputs of this block: codes c0..c0+255, all records
+    for (int64_t i = threadIdx.x; i < total; i += 256) {
+        const int64_t c = c0 + i / p.n, s = i % p.n;  // consecutive threads -> consecutive records
+        if (c < nbins) p.sum[s + p.ld * c] = (int32_t)p.stage[s * nbins + c];
+    }
+}
+
+// invalid[s] = windows in range - sum of the record's bucket counts
+template <int K, class Idx>
+__global__ __launch_bounds__(256) void radix_invalid_kernel(RParams p) {
+    const int64_t s = blockIdx.x;
+    const int64_t m = (int64_t)p.nbk * p.G;
+    uint64_t acc = 0;
+    for (int64_t i = threadIdx.x; i < m; i += 256) acc += p.cnt[s * m + i];
+    __shared__ uint64_t red[256];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const Geom g = make_geom<Idx>(p);
+        int64_t ca, ce;
+        record_windows<K, Idx>(p, g, s, ca, ce);
+        const int64_t nw = ce > ca ? ce - ca : 0;
+        p.invalid[s] = (int32_t)(nw - (int64_t)red[0]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host
+// ---------------------------------------------------------------------------
+constexpr int kPassBlock = 512;
+
+inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct RLayout {
+    size_t cnt, off, bsum, ent, stage, total;
+    int64_t m, nscan;
+};
+
+inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap) {
+    RLayout L;
+    const int64_t nbk = (int64_t)1 << (2 * k - kLowBits);
+    L.m = n * nbk * G;
+    L.nscan = (L.m + kScanTile - 1) / kScanTile;
+    size_t o = 0;
+    L.cnt = o;
+    o += al256((size_t)L.m * 4);
+    L.off = o;
+    o += al256((size_t)(L.m + 1) * 8);
+    L.bsum = o;
+    o += al256((size_t)(L.nscan + 1) * 8);
+    L.ent = o;
+    o += al256((size_t)ent_cap * 2 + 16);
+    L.stage = o;
+    o += al256((size_t)n * ((size_t)1 << (2 * k)) * 4);
+    L.total = o;
+    return L;
+}
+
+std::mutex r_mu;
+int r_cus = 0, r_occ = 0;
+
+int r_grid(int device, int &G) {
+    std::lock_guard<std::mutex> lk(r_mu);
+    if (r_cus == 0) {
+        hipError_t e = hipDeviceGetAttribute(&r_cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e != hipSuccess) return (int)e;
+        int nb = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void *>(&radix_pass_kernel<13, int64_t, true, kPassBlock>), kPassBlock, 0);
+        if (e != hipSuccess) return (int)e;
+        r_occ = nb > 0 ? nb : 1;
+    }
+    G = r_cus * r_occ;
+    return 0;
+}
+
+struct RCache {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+std::vector<RCache> r_ws;
+
+template <int K>
+int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out) {
+    int device = 0;
+    hipError_t he = hipGetDevice(&device);
+    if (he != hipSuccess) return (int)he;
+    int G = 0;
+    int e = r_grid(device, G);
+    if (e) return e;
+    const int64_t wl = (int64_t)a->win_lo, wh = (int64_t)a->win_hi;
+    const int64_t tiles = wh > wl ? ((wh + kTile - 1) >> kTileShift) - (wl >> kTileShift) : 0;
+    if (tiles < G) G = tiles > 0 ? (int)tiles : 1;
+    const int64_t n = (int64_t)a->num_seqs;
+    const int64_t ent_cap = wh > wl ? wh - wl : 0;  // >= valid windows in range
+    const RLayout L = r_layout(K, n, G, ent_cap);
+    if (size_only) {
+        *size_out = L.total;
+        return 0;
+    }
+    void *ws = a->workspace;
+    if (ws == nullptr) {
+        std::lock_guard<std::mutex> lk(r_mu);
+        if ((int)r_ws.size() <= device) r_ws.resize(device + 1);
+        RCache &c = r_ws[device];
+        if (c.bytes < L.total) {
+            if (c.ptr) {
+                he = hipFree(c.ptr);
+                if (he != hipSuccess) return (int)he;
+            }
+            c.ptr = nullptr;
+            c.bytes = 0;
+            if (hipMalloc(&c.ptr, L.total) != hipSuccess) return KMC_ERR_NOMEM;
+            c.bytes = L.total;
+        }
+        ws = c.ptr;
+    } else if (a->workspace_bytes < L.total) {
+        return KMC_ERR_WORKSPACE;
+    }
+    char *base = static_cast<char *>(ws);
+    RParams p;
+    p.data = a->data;
+    p.indices = a->indices;
+    p.n = n;
+    p.wl = wl;
+    p.wh = wh;
+    p.rl = (int64_t)a->read_lo;
+    p.rh = (int64_t)a->read_hi;
+    p.derive = 0;
+    p.G = G;
+    p.nbk = 1 << (2 * K - kLowBits);
+    p.cnt = reinterpret_cast<uint32_t *>(base + L.cnt);
+    p.off = reinterpret_cast<uint64_t *>(base + L.off);
+    p.ent = reinterpret_cast<uint16_t *>(base + L.ent);
+    p.stage = reinterpret_cast<uint32_t *>(base + L.stage);
+    p.sum = a->sum;
+    p.ld = a->sum_ld ? (int64_t)a->sum_ld : n;
+    p.invalid = a->invalid;
+    uint64_t *bsum = reinterpret_cast<uint64_t *>(base + L.bsum);
+    const int64_t nbins = (int64_t)1 << (2 * K);
+
+    he = hipMemsetAsync(p.cnt, 0, (size_t)L.m * 4, st);
+    if (he != hipSuccess) return (int)he;
+    hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, false, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)L.nscan), dim3(kScanBlock), 0, st, p.cnt, L.m, bsum);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kScanBlock), 0, st, bsum, L.nscan);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)L.nscan), dim3(kScanBlock), 0, st, p.cnt, L.m, bsum,
+                       p.off);
+    hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, true, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
+    hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)(n * p.nbk)), dim3(1024), 0, st, p, nbins);
+    hipLaunchKernelGGL(radix_place_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st, p, nbins);
+    if (a->invalid)
+        hipLaunchKernelGGL((radix_invalid_kernel<K, int64_t>), dim3((unsigned)n), dim3(256), 0, st, p);
+    he = hipGetLastError();
+    return (int)he;
+}
+
+}  // namespace
+
+// Entry used by kmc_dense.hip for 9 <= k <= KMC_DENSE_MAX_K.
+int radix_dense(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out) {
+    switch (a->k) {
+        case 9: return run_radix<9>(a, st, size_only, size_out);
+        case 10: return run_radix<10>(a, st, size_only, size_out);
+        case 11: return run_radix<11>(a, st, size_only, size_out);
+        case 12: return run_radix<12>(a, st, size_only, size_out);
+        case 13: return run_radix<13>(a, st, size_only, size_out);
+        default: return KMC_ERR_UNSUPPORTED_K;
+    }
+}
+
+}  // namespace kmc

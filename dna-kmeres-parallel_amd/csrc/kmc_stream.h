@@ -1,0 +1,293 @@
+// kmc_stream.h — the tile streaming loop shared by the HIP counting kernels.
+//
+// One wave streams a contiguous run of 1 KiB tiles of the ASCII record buffer
+// (64 lanes x 16 B, global_load_dwordx4), decodes each lane's 16 bytes to 2-bit
+// codes in registers, attaches the next lane's 16 bases as the (k-1)-base halo
+// (lane 63: lane 0 of the next tile, already prefetched), and hands every tile
+// to an operation functor: op.tile<MASKED>(lo, hi, W) with lo = the lane's 16
+// bases, hi = the next 16, W = 16-bit mask of the windows to count (MASKED ==
+// false: all 16).  The functor decides what a window does (LDS histogram add,
+// bucket count, bucket scatter, ...).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+// Tiles kept in flight per wave ahead of the one being counted, and whether the
+// once-read sequence stream uses non-temporal (nt) loads (diagnostic knobs).
+#ifndef KMC_PF
+#define KMC_PF 2
+#endif
+#ifndef KMC_NT
+#define KMC_NT 0
+#endif
+// Diagnostic builds only (scripts/kbench.py): KMC_ABLATE=1 replaces the
+// per-window work by a register XOR (codes still computed), KMC_ABLATE=2 also
+// skips the decode (loads only).  The shipped library is built with KMC_ABLATE=0.
+#ifndef KMC_ABLATE
+#define KMC_ABLATE 0
+#endif
+
+namespace kmc {
+
+constexpr int kTileShift = 10;  // 1 KiB per wave per tile
+constexpr int kTile = 1 << kTileShift;
+
+// ---------------------------------------------------------------------------
+// decode: 16 ASCII bytes (one lane's chunk) -> 32-bit word of 2-bit codes, base i
+// at bits 2i (the reference's little-endian bin order), plus validity.
+//
+// The low 3 bits of A,C,G,T are 1,3,7,4 and distinct, so one v_perm_b32 on
+// (w & 0x07070707) maps every byte to its code (a 4-entry table lookup per
+// byte) and a second one to the letter that code stands for; a byte is valid
+// iff it equals that letter (lowercase, N, '\r', '\0', ... never do).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kCodeLo = 0x01000000u;   // table[0..3] = {-, A=0, -, C=1}
+constexpr uint32_t kCodeHi = 0x02000003u;   // table[4..7] = {T=3, -, -, G=2}
+constexpr uint32_t kCanonLo = 0x43FF41FFu;  // table[0..3] = {xx, 'A', xx, 'C'}
+constexpr uint32_t kCanonHi = 0x47FFFF54u;  // table[4..7] = {'T', xx, xx, 'G'}
+
+__device__ __forceinline__ uint32_t byte_codes(uint32_t w) {
+    return __builtin_amdgcn_perm(kCodeHi, kCodeLo, w & 0x07070707u);
+}
+__device__ __forceinline__ uint32_t byte_mismatch(uint32_t w) {  // 0 in every valid byte
+    return w ^ __builtin_amdgcn_perm(kCanonHi, kCanonLo, w & 0x07070707u);
+}
+
+// code = 16 packed 2-bit codes; bad = OR of the per-byte mismatches (0 iff all valid)
+__device__ __forceinline__ void decode16(const uint4 r, uint32_t &code, uint32_t &bad) {
+    const uint32_t c0 = byte_codes(r.x), c1 = byte_codes(r.y), c2 = byte_codes(r.z), c3 = byte_codes(r.w);
+    bad = byte_mismatch(r.x) | byte_mismatch(r.y) | byte_mismatch(r.z) | byte_mismatch(r.w);
+    // bytes -> nibbles -> one byte per dword (base 4d+i at bits 2(4d+i))
+    const uint32_t u = __builtin_amdgcn_perm(c1, c0, 0x06040200u) | (__builtin_amdgcn_perm(c1, c0, 0x07050301u) << 2);
+    const uint32_t v = __builtin_amdgcn_perm(c3, c2, 0x06040200u) | (__builtin_amdgcn_perm(c3, c2, 0x07050301u) << 2);
+    code = __builtin_amdgcn_perm(v, u, 0x06040200u) | (__builtin_amdgcn_perm(v, u, 0x07050301u) << 4);
+}
+
+// 16-bit invalid-base mask of a chunk (slow path only)
+__device__ __forceinline__ uint32_t bad_mask16(const uint4 r) {
+    const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    uint32_t bad = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t x = byte_mismatch(w[d]);
+        const uint32_t nz = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        bad |= ((((nz >> 7) * 0x00204081u) >> 21) & 0xFu) << (4 * d);
+    }
+    return bad;
+}
+
+// One lane's 16 bytes of tile t; bytes outside [rl, rh) read as 0 (invalid).
+__device__ __forceinline__ uint4 load_lane(const char *__restrict__ data, int64_t t, int lane, int64_t rl,
+                                           int64_t rh) {
+    const int64_t base = t << kTileShift;
+    const int64_t q = base + (int64_t)lane * 16;
+    if (base >= rl && base + kTile <= rh) {  // wave-uniform: whole tile readable
+#if KMC_NT
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(data + q));
+        return make_uint4(x[0], x[1], x[2], x[3]);
+#else
+        return *reinterpret_cast<const uint4 *>(data + q);
+#endif
+    }
+    uint32_t v[4] = {0u, 0u, 0u, 0u};
+    if (q >= rl && q + 16 <= rh) {
+        const uint4 x = *reinterpret_cast<const uint4 *>(data + q);
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else {
+#pragma unroll 1
+        for (int i = 0; i < 16; ++i) {
+            const int64_t b = q + i;
+            if (b >= rl && b < rh) v[i >> 2] |= (uint32_t)(uint8_t)data[b] << (8 * (i & 3));
+        }
+    }
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// OR of x >> 0 .. x >> (K-1): bit j set iff any of bases j .. j+K-1 is invalid.
+template <int K>
+__device__ __forceinline__ uint32_t smear(uint32_t x) {
+    uint32_t s = x;
+    int c = 1;
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+        if (c < K) {
+            const int st = (c < K - c) ? c : (K - c);
+            s |= s >> st;
+            c += st;
+        }
+    }
+    return s;
+}
+
+// Value of lane+1 (lane 63 gets 0): DPP wave_shl:1, no LDS traffic (unlike
+// __shfl_down, which is a ds_bpermute).
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for
+// the wave's outstanding global loads, so the tile prefetch keeps streaming.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Geometry of a counting launch.  P carries indices, n, derive, wl/wh/rl/rh, G.
+struct Geom {
+    int64_t wl, wh, rl, rh;
+    int64_t T0, T1, tpw;
+};
+
+template <class Idx, class P>
+__device__ __forceinline__ int64_t rec_off(const P &p, int64_t i) {
+    return (int64_t)((const Idx *)p.indices)[i];
+}
+
+template <class Idx, class P>
+__device__ __forceinline__ Geom make_geom(const P &p) {
+    Geom g;
+    if (p.derive) {
+        g.wl = rec_off<Idx>(p, 0);
+        g.wh = rec_off<Idx>(p, p.n);
+        g.rl = g.wl;
+        g.rh = g.wh;
+    } else {
+        g.wl = p.wl;
+        g.wh = p.wh;
+        g.rl = p.rl;
+        g.rh = p.rh;
+    }
+    if (g.wh <= g.wl) {
+        g.T0 = g.T1 = 0;
+        g.tpw = 1;
+    } else {
+        g.T0 = g.wl >> kTileShift;
+        g.T1 = (g.wh + kTile - 1) >> kTileShift;
+        g.tpw = (g.T1 - g.T0 + p.G - 1) / p.G;
+    }
+    return g;
+}
+
+// Window range of record s clipped to the counted range: [ca, ce).
+template <int K, class Idx, class P>
+__device__ __forceinline__ void record_windows(const P &p, const Geom &g, int64_t s, int64_t &ca,
+                                               int64_t &ce) {
+    const int64_t a = rec_off<Idx>(p, s);
+    const int64_t e = rec_off<Idx>(p, s + 1);
+    const int64_t nw = e - a - K > 0 ? e - a - K : 0;  // kernels.h:133 generalised
+    ca = a > g.wl ? a : g.wl;
+    ce = (a + nw) < g.wh ? (a + nw) : g.wh;
+}
+
+
+// Last record s with indices[s] <= pos (records before it end at or before pos).
+template <class Idx, class P>
+__device__ __forceinline__ int64_t first_record_at(const P &p, int64_t pos) {
+    int64_t lo = 0, hi = p.n - 1;
+    if (rec_off<Idx>(p, 0) <= pos) {
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (rec_off<Idx>(p, mid) <= pos) lo = mid;
+            else hi = mid - 1;
+        }
+    }
+    return lo;
+}
+
+// One wave streams tiles [t0, t1) and counts the windows that start in [ps, pe),
+// over `per` workgroup-uniform iterations (waves with fewer tiles keep calling
+// op.after_iter, so workgroup barriers inside it stay matched).  Tiles are
+// streamed KMC_PF ahead; the decode of tile t+1 doubles as lane 63's halo of t.
+template <int K, class Op>
+__device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
+                                             int64_t ps, int64_t pe, int64_t rl, int64_t rh, int lane, Op &op) {
+    constexpr int PF = KMC_PF;  // r[0] = tile t, r[i] = tile t+i
+    uint4 r[PF + 1];
+#pragma unroll
+    for (int q = 0; q <= PF; ++q) r[q] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t c_cur = 0u, v_cur = 0u;
+    if (t0 < t1) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q)
+            if (t0 + q <= t1) r[q] = load_lane(data, t0 + q, lane, rl, rh);
+#if KMC_ABLATE == 2
+        c_cur = r[0].x ^ r[0].y;
+#else
+        decode16(r[0], c_cur, v_cur);
+#endif
+    }
+    for (int64_t i = 0; i < per; ++i) {
+        const int64_t t = t0 + i;
+        if (t < t1) {
+            r[PF] = make_uint4(0u, 0u, 0u, 0u);
+            if (t + PF <= t1) r[PF] = load_lane(data, t + PF, lane, rl, rh);
+            const uint4 r_cur = r[0], r_nxt = r[1];
+            uint32_t c_nxt, v_nxt;
+#if KMC_ABLATE == 2
+            c_nxt = r_nxt.x ^ r_nxt.y ^ r_nxt.z ^ r_nxt.w;
+            v_nxt = 0u;
+#else
+            decode16(r_nxt, c_nxt, v_nxt);
+#endif
+            // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
+            uint32_t hc = from_next_lane(c_cur);
+            uint32_t hv = from_next_lane(v_cur);
+            const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
+            const uint32_t v0 = __builtin_amdgcn_readlane(v_nxt, 0);
+            if (lane == 63) {
+                hc = c0;
+                hv = v0;
+            }
+            op.before_tile();
+            const int64_t base = t << kTileShift;
+            const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
+            if (interior && !__any((v_cur | hv) != 0u)) {
+#if KMC_ABLATE == 0
+                op.template tile<false>(c_cur, hc, 0xFFFFu);
+#else
+                asm volatile("" ::"v"(c_cur), "v"(hc));
+#endif
+            } else {
+                // boundary tile or invalid bytes: exact per-window mask
+                const int64_t pos = base + (int64_t)lane * 16;
+                const int64_t dlo = ps - pos, dhi = pe - pos;
+                const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
+                const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
+                const uint32_t b_own = bad_mask16(r_cur);
+                uint32_t b_next = from_next_lane(b_own);
+                const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
+                if (lane == 63) b_next = b0;
+                const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
+#if KMC_ABLATE == 0
+                op.template tile<true>(c_cur, hc, W);
+#else
+                asm volatile("" ::"v"(c_cur), "v"(hc), "v"(W));
+#endif
+            }
+#pragma unroll
+            for (int q = 0; q < PF; ++q) r[q] = r[q + 1];
+            c_cur = c_nxt;
+            v_cur = v_nxt;
+        }
+        op.after_iter(i, per, t < t1);
+    }
+}
+
+// Code of window j (bases j .. j+K-1, K <= 16) of a lane with bases lo : hi.
+template <int K>
+__device__ __forceinline__ uint32_t window_code_rt(uint32_t lo, uint32_t hi, int j) {
+    constexpr uint32_t M = (K >= 16) ? 0xFFFFFFFFu : ((1u << (2 * K)) - 1u);
+    return __builtin_amdgcn_alignbit(hi, lo, 2 * j) & M;
+}
+
+}  // namespace kmc

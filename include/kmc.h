@@ -41,7 +41,7 @@ typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedef */
 #endif
 
 /* Largest k of the dense (4^k-bin) histogram path. */
-#define KMC_DENSE_MAX_K 8
+#define KMC_DENSE_MAX_K 13
 
 /* Reference loader cap (main.cu:30). */
 #define KMC_MAX_SEQS_REFERENCE 100

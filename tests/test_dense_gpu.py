@@ -59,8 +59,6 @@ def test_dense_matches_golden(kmc, cuda, name, dialect):
     idx = G.full_indices(g)
     for k in g["ks"]:
         k = int(k)
-        if k > 8:
-            continue
         got, inv = run_dense(kmc, cuda, g["data"], idx, k)
         exp, exp_inv = G.dense_expected(g, k)
         np.testing.assert_array_equal(got, exp, err_msg="%s/%s k=%d" % (name, dialect, k))
@@ -113,6 +111,39 @@ def test_dense_random_vs_oracle(kmc, oracle, cuda, k):
     exp, exp_inv = oracle.count_dense(data, idx, k)
     np.testing.assert_array_equal(got, exp)
     np.testing.assert_array_equal(inv, exp_inv)
+
+
+@pytest.mark.parametrize("k", [9, 10, 11, 12, 13])
+def test_radix_k9_13_vs_oracle(kmc, oracle, cuda, k):
+    """9 <= k <= 13: the radix-partitioned path (67 M bins per record at k = 13)."""
+    rng = np.random.default_rng(2000 + k)
+    lens = [0, 1, k - 1, k, k + 1, 1025, 300_000, 17, 2_000_003]
+    data, idx = random_records(rng, lens, 0.003, 0.003, 0.001)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
+@pytest.mark.parametrize("k", [11, 13])
+def test_radix_shards_sum_to_full(kmc, oracle, cuda, k):
+    import torch
+    rng = np.random.default_rng(31 + k)
+    data, idx = random_records(rng, [600_000, 5, 400_001], 0.002, 0.002)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    acc = np.zeros_like(exp)
+    inv_acc = np.zeros_like(exp_inv)
+    for a, b, rl, rh in kmc.plan_shards(idx, k, 3):
+        out = torch.full((1 << (2 * k), idx.size - 1), -1, dtype=torch.int32, device=cuda)
+        inv = torch.full((idx.size - 1,), -1, dtype=torch.int32, device=cuda)
+        kmc.count_dense_ex(kmc.dense_args(d, di, k, out, read=(rl, rh), win=(a, b), invalid=inv))
+        torch.cuda.synchronize()
+        acc += out.cpu().numpy()
+        inv_acc += inv.cpu().numpy()
+        del out
+    np.testing.assert_array_equal(acc, exp)
+    np.testing.assert_array_equal(inv_acc, exp_inv)
 
 
 @pytest.mark.parametrize("k", [3, 8])
