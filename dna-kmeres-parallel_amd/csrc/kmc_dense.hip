@@ -36,6 +36,8 @@
 #include "kmc_stream.h"
 
 namespace kmc {
+thread_local hipEvent_t t_trace_before = nullptr;
+thread_local hipEvent_t t_trace_after = nullptr;
 namespace {
 
 struct Spill {
@@ -561,8 +563,6 @@ struct DevInfo {
 std::mutex g_mu;
 std::vector<DevInfo> g_dev;
 
-thread_local hipEvent_t t_trace_before = nullptr;
-thread_local hipEvent_t t_trace_after = nullptr;
 
 template <int K, class Idx>
 void *kernel_ptr() {

@@ -6,6 +6,11 @@ struct kmc_dense_args;
 typedef struct ihipStream_t *hipStream_t;
 
 namespace kmc {
+typedef struct ihipEvent_t *hipEvent_t;
+// kmc_trace_set_events: recorded around the histogram kernel (k <= 8) or the
+// whole radix pipeline (k > 8) of the next dense count calls on this thread.
+extern thread_local hipEvent_t t_trace_before, t_trace_after;
+
 // 9 <= k <= KMC_DENSE_MAX_K: radix-partitioned dense counting (kmc_radix.hip).
 // size_only: report the workspace size in *size_out instead of launching.
 int radix_dense(const ::kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out);

@@ -395,6 +395,10 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     uint64_t *bsum = reinterpret_cast<uint64_t *>(base + L.bsum);
     const int64_t nbins = (int64_t)1 << (2 * K);
 
+    if (t_trace_before) {
+        he = hipEventRecord(t_trace_before, st);
+        if (he != hipSuccess) return (int)he;
+    }
     he = hipMemsetAsync(p.cnt, 0, (size_t)L.m * 4, st);
     if (he != hipSuccess) return (int)he;
     hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, false, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
@@ -405,6 +409,10 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, true, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
     hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)(n * p.nbk)), dim3(1024), 0, st, p, nbins);
     hipLaunchKernelGGL(radix_place_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st, p, nbins);
+    if (t_trace_after) {
+        he = hipEventRecord(t_trace_after, st);
+        if (he != hipSuccess) return (int)he;
+    }
     if (a->invalid)
         hipLaunchKernelGGL((radix_invalid_kernel<K, int64_t>), dim3((unsigned)n), dim3(256), 0, st, p);
     he = hipGetLastError();

@@ -42,9 +42,11 @@ def main():
         with open(os.path.join(DST, "%s_bench_trace.json" % tag), "w") as fh:
             json.dump(line, fh, indent=1)
     k = line["config"]["k"] if line else 8
-    kern = "count_dense_kernel<%d," % k
+    kern = "count_dense_kernel<%d, 1, 3," % k if k == 8 else "count_dense_kernel<%d," % k
     fetch = per_launch(os.path.join(SRC, "fetch"), "FETCH_SIZE", kern)
     write = per_launch(os.path.join(SRC, "write"), "WRITE_SIZE", kern)
+    r128 = per_launch(os.path.join(SRC, "fetch"), "TCC_EA0_RDREQ_128B", kern)
+    r64 = per_launch(os.path.join(SRC, "fetch"), "TCC_EA0_RDREQ_64B", kern)
     if fetch and write and line:
         f = sum(fetch) / len(fetch)
         w = sum(write) / len(write)
@@ -55,10 +57,14 @@ def main():
             "fetch_size_kib_per_launch": f,
             "write_size_kib_per_launch": w,
             "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
-            "correction": "gfx950: FETCH_SIZE x2 for 16-B/lane streaming reads (MI355X_MICROARCH.md HBM section)",
+            "correction": "gfx950: FETCH_SIZE counts a 128-B read request as 64 B (x2; MI355X_MICROARCH.md HBM "
+                          "section), confirmed here by TCC_EA0_RDREQ_128B x 128 B",
             "launches_sampled": [len(fetch), len(write)],
-            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) of python3 bench.py --steps 3",
+            "source": "rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_64B / --pmc WRITE_SIZE "
+                      "(separate passes) of python3 bench.py --steps 3",
         }
+        if r128:
+            out["rdreq_bytes_per_launch"] = (sum(r128) / len(r128)) * 128 + (sum(r64) / len(r64) if r64 else 0) * 64
         with open(os.path.join(DST, "pmc_dense_k8_10gbase.json"), "w") as fh:
             json.dump(out, fh, indent=1)
         print(json.dumps(out))
