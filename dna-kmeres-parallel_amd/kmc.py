@@ -86,6 +86,10 @@ def lib():
         L.kmc_fasta_data.argtypes = [_P]
         L.kmc_fasta_free.argtypes = [_P]
         L.kmc_fasta_free.restype = None
+        L.kmc_pair_distances_workspace_size.restype = ctypes.c_size_t
+        L.kmc_pair_distances_workspace_size.argtypes = [_U64, ctypes.c_int, ctypes.c_int]
+        L.kmc_pair_distances.argtypes = [_P, _U64, _P, _U64, ctypes.c_int, _P, _P, ctypes.c_size_t, _P]
+        L.minKmeres2_hip.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P, _P]
         _lib = L
     return _lib
 
@@ -184,6 +188,33 @@ def count_dense_ex(args, stream=None):
 
 def dense_ex_workspace_size(args, device=0):
     return int(lib().kmc_count_dense_ex_workspace_size(ctypes.byref(args), device))
+
+
+def pair_distances_workspace_size(num_seqs, k, device=0):
+    return int(lib().kmc_pair_distances_workspace_size(num_seqs, k, device))
+
+
+def pair_distances(counts, indices, k, num_seqs=None, ld=0, out=None, workspace=None, stream=None):
+    """All-pairs k-mer distance (kmc_pair_distances): `counts` is the int32 count
+    matrix sum[s + ld*code] (e.g. count_dense's (4^k, n) tensor), `indices` the
+    device int64 offsets.  Returns float32 [n(n-1)/2], packed upper triangle."""
+    import torch
+    n = int(num_seqs if num_seqs is not None else indices.numel() - 1)
+    if out is None:
+        out = torch.empty(max(n * (n - 1) // 2, 0), dtype=torch.float32, device=counts.device)
+    ws_ptr, ws_bytes = None, 0
+    if workspace is not None:
+        ws_ptr, ws_bytes = _dptr(workspace), workspace.numel() * workspace.element_size()
+    rc = lib().kmc_pair_distances(_dptr(counts), ld, _dptr(indices), n, k, _dptr(out), ws_ptr, ws_bytes,
+                                  _stream(stream))
+    _check(rc, "kmc_pair_distances")
+    return out
+
+
+def min_kmeres2(sums, mins, num_seqs, current_seq, indexes, stream=None):
+    """Drop-in of one reference minKmeres2 launch (k = 3, int32 indexes)."""
+    rc = lib().minKmeres2_hip(_dptr(sums), _dptr(mins), num_seqs, current_seq, _dptr(indexes), _stream(stream))
+    _check(rc, "minKmeres2_hip")
 
 
 def trace_events(before=None, after=None):

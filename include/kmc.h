@@ -142,6 +142,36 @@ int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs,
                     int ndev, const int *devices, int32_t *sum, int32_t *invalid);
 
 /* ------------------------------------------------------------------------ */
+/* Pairwise k-mer distance (the reference's step 2).
+ * For every pair of records i < j:
+ *     d(i,j) = 1 - (float)S_ij / (float)(min(len_i, len_j) - k + 1)
+ *     S_ij   = sum over the 4^k codes of min(sum[i + ld*code], sum[j + ld*code])
+ *     len_s  = indices[s+1] - indices[s] - 1
+ * written to out[n*i - i*(i-1)/2 + (j-i) - (i+1)], the packed upper triangle of
+ * getIdxTriangularMatrixRowMajor(i+1, j-i, n) (kernels.h:46-48), n(n-1)/2 floats.
+ * S_ij is summed exactly in 64-bit integers, so the result is that of the CPU
+ * path (sequentialKmerCount2, main.cu:604-619) bit for bit; it replaces the host
+ * loop of num_seqs minKmeres2 launches (main.cu:326-335) with one launch.
+ *   sum       device int32 count matrix of kmc_count_dense (row stride sum_ld,
+ *             0 -> num_seqs); counts are taken as unsigned
+ *   indices   device int64[num_seqs + 1]
+ *   out       device float[num_seqs*(num_seqs-1)/2]
+ *   workspace device scratch of kmc_pair_distances_workspace_size() bytes (0 when
+ *             the pair matrix alone fills the GPU), or NULL for a library buffer
+ * Exact while every record has fewer than 2^32 windows. */
+size_t kmc_pair_distances_workspace_size(uint64_t num_seqs, int k, int device);
+int kmc_pair_distances(const int32_t *sum, uint64_t sum_ld, const int64_t *indices, uint64_t num_seqs, int k,
+                       float *out, void *workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* Exact drop-in for one reference launch
+ *     minKmeres2<<<blocks, threads>>>(sums, mins, num_seqs, current_seq, indexes)
+ * (kernels.h:85-109, launched per row at main.cu:327): the distances of record
+ * current_seq to every later record, 4^KMC_DROPIN_K codes, summed in float in
+ * code order as kernels.h:103 does (so bit-identical to the reference kernel
+ * also when that float sum rounds).  Device int sums/indexes, float mins. */
+int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq, int *indexes, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Tracing (the reference times step 1 with cudaEvents, main.cu:262-300): when set,
  * every following dense count call on this host thread records `before` right
  * before its histogram kernel and `after` right after it, on the call's stream,

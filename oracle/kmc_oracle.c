@@ -167,3 +167,25 @@ void oracle_pair_distances(const int32_t *sum, const int64_t *lens, int64_t n, i
         }
     }
 }
+
+/*
+ * One launch of the reference's GPU step 2, minKmeres2 (kernels.h:85-109): row
+ * `cur` against every later record, the sum of minima accumulated in FLOAT in code
+ * order (kernels.h:102-104), the lengths from int offsets (kernels.h:99-101).
+ * counts in GPU layout sum[s + n*code], nbins = 4^k codes.  Writes only the
+ * entries of row `cur` of the packed triangle.
+ */
+void oracle_min_kmeres2_row(const int32_t *sum, const int32_t *indexes, int n, int cur, int k, float *out) {
+    const int nbins = 1 << (2 * k);
+    for (int j = cur + 1; j < n; ++j) {
+        float s = 0;
+        for (int p = 0; p < nbins; ++p) {
+            int32_t a = sum[cur + (int64_t)n * p], b = sum[j + (int64_t)n * p];
+            s += (float)(a < b ? a : b);
+        }
+        int le = indexes[cur + 1] - indexes[cur] - 1, lc = indexes[j + 1] - indexes[j] - 1;
+        if (le < lc) lc = le;
+        s = 1 - s / (float)(lc - k + 1);
+        out[tri_idx(cur + 1, j - cur, n)] = s;
+    }
+}

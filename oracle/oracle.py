@@ -47,6 +47,7 @@ def lib():
         L.oracle_window_code.argtypes = [ctypes.c_char_p, ctypes.c_int]
         L.oracle_window_code.restype = _I64
         L.oracle_pair_distances.argtypes = [_P, _P, _I64, ctypes.c_int, _P]
+        L.oracle_min_kmeres2_row.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
         _lib = L
     return _lib
 
@@ -78,6 +79,17 @@ def pair_distances(sum_, lens, k):
     out = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float32)
     lib().oracle_pair_distances(_ptr(sum_), _ptr(lens), n, k, _ptr(out))
     return out[: n * (n - 1) // 2]
+
+
+def min_kmeres2_row(sum_, indexes, cur, k, out=None):
+    """GPU step-2 semantics (float accumulation) for row `cur`; fills `out`."""
+    sum_ = np.ascontiguousarray(sum_, dtype=np.int32)
+    indexes = np.ascontiguousarray(indexes, dtype=np.int32)
+    n = indexes.size - 1
+    if out is None:
+        out = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float32)
+    lib().oracle_min_kmeres2_row(_ptr(sum_), _ptr(indexes), n, cur, k, _ptr(out))
+    return out
 
 
 def py_count_record(rec: bytes, k: int):
@@ -135,6 +147,17 @@ def ref_import(path, nonl=False):
     return n, np.array(idx[:ni], dtype=np.int64), np.frombuffer(buf.raw[:dsz], dtype=np.uint8).copy()
 
 
+def ref_seq_distances(path, k, nonl=False):
+    """sequentialKmerCount2 (main.cu:587-621) on the file's records, as imported by
+    the reference loader: packed upper-triangle float32 distances."""
+    L = ref_cpu()
+    n, _, _ = ref_import(path, nonl)
+    out = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float32)
+    L.ref_seq_distances.argtypes = [ctypes.c_int, _P]
+    L.ref_seq_distances(k, _ptr(out))
+    return out[: n * (n - 1) // 2]
+
+
 def ref_count_bytes(rec: np.ndarray, k: int):
     """permutationsCountAll on one record (bytes incl. terminator): CPU layout."""
     L = ref_cpu()
@@ -157,5 +180,6 @@ def ref_kernel():
     if _ref_kernel is None:
         L = ctypes.CDLL(os.path.join(REF_DIR, "libref_kernel.so"))
         L.ref_kernel_launch.argtypes = [_P, _P, ctypes.c_uint, _P]
+        L.ref_min_kmeres2_launch.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P]
         _ref_kernel = L
     return _ref_kernel

@@ -11,6 +11,9 @@
 //   frag_import.inc       main.cu:474-530   importSeqs, up to the point where it
 //                                           allocates CUDA managed memory
 //   frag_import_nonl.inc  main.cu:401-458   importSeqsNoNL, same cut
+//   frag_dist.inc         main.cu:63, 118, 587-621, 671-673
+//                                           sequentialKmerCount2 (CPU pairwise
+//                                           distance) + its index helper/global
 //
 // The two import fragments stop right before `cudaError_t error;` (main.cu:531 /
 // main.cu:459): the rest of each function only copies globalAcc into a
@@ -33,6 +36,7 @@
 }                               // closes importSeqs (see header comment)
 #include "frag_import_nonl.inc" // importSeqsNoNL (body through main.cu:458)
 }                               // closes importSeqsNoNL
+#include "frag_dist.inc"        // sequentialKmerCount2, distancesSequential
 
 static int g_map_k = -1;
 
@@ -118,6 +122,16 @@ void ref_count_bytes(const char *bytes, long E, int k, int *out) {
     std::string seq(bytes, (size_t)E);
     if (E > 0) seq[E - 1] = '|';
     permutationsCountAll(seq, out, 1 << (2 * k), k);
+}
+
+// sequentialKmerCount2 (main.cu:587-621) over the imported records: the packed
+// upper triangle of distances, n(n-1)/2 floats, into `out`.
+void ref_seq_distances(int k, float *out) {
+    ref_build_map(k);
+    distancesSequential = out;
+    std::vector<std::string> unused;
+    sequentialKmerCount2(seqs, unused, k);
+    distancesSequential = nullptr;
 }
 
 }  // extern "C"

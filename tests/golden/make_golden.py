@@ -19,6 +19,8 @@ fixtures are data only: each <case>.<dialect>.npz holds
     ks              k values counted
     k{k}_rec/_code/_count   nonzero GPU-layout bins (record, LE code, count)
     k{k}_invalid    CPU bin 0 per record
+    k{k}_dist       sequentialKmerCount2's packed upper-triangle distances
+                    (main.cu:587-621), float32, n(n-1)/2 entries
 and patterns_k{k}.npy holds the bin-order table of permutation() for small k.
 """
 import ctypes
@@ -121,6 +123,7 @@ def main():
     lib.ref_num_indexes.restype = ctypes.c_long
     lib.ref_data_size.restype = ctypes.c_long
     lib.ref_record_size.restype = ctypes.c_long
+    lib.ref_seq_distances.argtypes = [ctypes.c_int, ctypes.c_void_p]
 
     for k in range(1, 6):
         buf = ctypes.create_string_buffer((1 << (2 * k)) * k)
@@ -162,6 +165,9 @@ def main():
                 out["k%d_code" % k] = np.concatenate(codes) if codes else np.zeros(0, np.int64)
                 out["k%d_count" % k] = np.concatenate(counts) if counts else np.zeros(0, np.int32)
                 out["k%d_invalid" % k] = np.array(invalid, dtype=np.int32)
+                dist = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float32)
+                lib.ref_seq_distances(k, dist.ctypes.data)
+                out["k%d_dist" % k] = dist[: n * (n - 1) // 2]
             np.savez_compressed(os.path.join(HERE, "%s.%s.npz" % (name, dialect)), **out)
             print("%-15s %-5s n=%3d indexes=%3d bytes=%d ks=%s" % (name, dialect, n, ni, dsz, ks))
 

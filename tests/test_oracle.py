@@ -77,3 +77,56 @@ def test_oracle_range_partition_sums(oracle):
         part, _ = oracle.count_dense(data, idx, 5, win=(a, b))
         acc += part
     np.testing.assert_array_equal(acc, full)
+
+
+# ---------------------------------------------------------------------------
+# pairwise distance (step 2)
+# ---------------------------------------------------------------------------
+def golden_lens(g):
+    idx = G.full_indices(g)
+    return np.diff(idx) - 1
+
+
+@pytest.mark.parametrize("name,dialect", G.cases())
+def test_oracle_distances_match_golden(oracle, name, dialect):
+    """oracle_pair_distances == sequentialKmerCount2 (main.cu:587-621) output."""
+    g = G.load(name, dialect)
+    for k in g["ks"]:
+        k = int(k)
+        exp, _ = G.dense_expected(g, k)
+        got = oracle.pair_distances(exp, golden_lens(g), k)
+        np.testing.assert_array_equal(got, g["k%d_dist" % k], err_msg="%s/%s k=%d" % (name, dialect, k))
+
+
+@pytest.mark.parametrize("name", ["basic", "maxseqs", "random"])
+def test_oracle_gpu_row_semantics_match_golden(oracle, name):
+    """The float-accumulating row function (minKmeres2, kernels.h:85-109) equals the
+    CPU path whenever its float sum is exact (small records)."""
+    g = G.load(name, "blank")
+    idx = G.full_indices(g).astype(np.int32)
+    exp, _ = G.dense_expected(g, 3)
+    n = idx.size - 1
+    out = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float32)
+    for cur in range(n):
+        oracle.min_kmeres2_row(exp, idx, cur, 3, out)
+    np.testing.assert_array_equal(out[: n * (n - 1) // 2], g["k3_dist"])
+
+
+def test_oracle_distances_match_reference_live(oracle, tmp_path):
+    """Random FASTA through the reference's own loader + sequentialKmerCount2."""
+    if not oracle.have_ref_cpu():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(31)
+    recs = []
+    for i in range(9):
+        L = int(rng.integers(1, 1500))
+        s = rng.choice(np.frombuffer(b"ACGTN", dtype=np.uint8), size=L, p=[.24, .24, .24, .24, .04])
+        recs.append(">x%d\n%s\n" % (i, s.tobytes().decode()))
+    fa = tmp_path / "d.fa"
+    fa.write_text("\n".join(recs).rstrip("\n"))
+    n, indexes, data = oracle.ref_import(str(fa))
+    idx = indexes if indexes.size == n + 1 else np.append(indexes, data.size)
+    for k in (2, 4, 6):
+        counts, _ = oracle.count_dense(data, idx, k)
+        got = oracle.pair_distances(counts, np.diff(idx) - 1, k)
+        np.testing.assert_array_equal(got, oracle.ref_seq_distances(str(fa), k))
