@@ -14,6 +14,7 @@ extern "C" const char *kmc_error_string(int code) {
         case KMC_ERR_NOMEM: return "allocation failed";
         case KMC_ERR_RCCL: return "RCCL call failed";
         case KMC_ERR_NO_DEVICE: return "no HIP device visible";
+        case KMC_ERR_CAPACITY: return "output capacity smaller than the result";
         default: return hipGetErrorString(static_cast<hipError_t>(code));
     }
 }

@@ -90,6 +90,8 @@ def lib():
         L.kmc_pair_distances_workspace_size.argtypes = [_U64, ctypes.c_int, ctypes.c_int]
         L.kmc_pair_distances.argtypes = [_P, _U64, _P, _U64, ctypes.c_int, _P, _P, ctypes.c_size_t, _P]
         L.minKmeres2_hip.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P, _P]
+        L.kmc_count_canonical_hash.argtypes = [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _P, _P, _U64, _P,
+                                               ctypes.POINTER(_U64), _P]
         _lib = L
     return _lib
 
@@ -209,6 +211,30 @@ def pair_distances(counts, indices, k, num_seqs=None, ld=0, out=None, workspace=
                                   _stream(stream))
     _check(rc, "kmc_pair_distances")
     return out
+
+
+CANON_SOFTMASK = 1
+CANON_FORWARD = 2
+CANON_MAX_K = 31
+
+
+def count_canonical(data, indices, k, flags=0, capacity=None, stream=None):
+    """Canonical k-mer counts per record (kmc_count_canonical_hash): returns
+    (keys uint64 as int64 tensor, counts int32 tensor, rec_offsets int64 tensor);
+    record s owns [rec_offsets[s], rec_offsets[s+1]), order within it unspecified."""
+    import torch
+    n = indices.numel() - 1
+    if capacity is None:
+        capacity = max(int(data.numel()), 1)
+    keys = torch.empty(capacity, dtype=torch.int64, device=data.device)
+    counts = torch.empty(capacity, dtype=torch.int32, device=data.device)
+    off = torch.zeros(max(n + 1, 1), dtype=torch.int64, device=data.device)
+    tot = _U64(0)
+    rc = lib().kmc_count_canonical_hash(_dptr(data), _dptr(indices), n, k, flags, _dptr(keys), _dptr(counts),
+                                        capacity, _dptr(off), ctypes.byref(tot), _stream(stream))
+    _check(rc, "kmc_count_canonical_hash")
+    t = int(tot.value)
+    return keys[:t], counts[:t], off
 
 
 def min_kmeres2(sums, mins, num_seqs, current_seq, indexes, stream=None):

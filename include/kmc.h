@@ -55,7 +55,8 @@ enum kmc_status {
     KMC_ERR_IO = 1005,            /* file cannot be opened/read */
     KMC_ERR_NOMEM = 1006,         /* host or device allocation failed */
     KMC_ERR_RCCL = 1007,          /* RCCL call failed */
-    KMC_ERR_NO_DEVICE = 1008      /* no HIP device visible */
+    KMC_ERR_NO_DEVICE = 1008,     /* no HIP device visible */
+    KMC_ERR_CAPACITY = 1009       /* caller output smaller than the result (size reported) */
 };
 
 /* Human-readable text for a kmc_status or hipError_t code (static storage). */
@@ -170,6 +171,33 @@ int kmc_pair_distances(const int32_t *sum, uint64_t sum_ld, const int64_t *indic
  * code order as kernels.h:103 does (so bit-identical to the reference kernel
  * also when that float sum rounds).  Device int sums/indexes, float mins. */
 int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq, int *indexes, hipStream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Canonical k-mer counting, k <= 31 (BASELINE config C4).  No
+ * reference counterpart (the reference's dense tables stop being feasible past
+ * k ~ 13); window and record rules are the dense path's (windows i < len_s - k + 1
+ * of each record, bytes other than A/C/G/T invalid).  Key of a valid window: its
+ * 2-bit encoding A0 C1 G2 T3 with the FIRST base MOST significant (so key order is
+ * lexicographic order), replaced by the key of its reverse complement when that is
+ * smaller.  Flags:
+ *   KMC_CANON_SOFTMASK  lowercase a/c/g/t count as their bases (soft-masked genomes)
+ *   KMC_CANON_FORWARD   no reverse-complement folding (key = the window itself;
+ *                       for k <= 13 these counts equal the dense histogram)
+ * Output, per record s: the distinct keys of s and their counts in
+ * keys/counts[rec_offsets[s] .. rec_offsets[s+1]) (order within a record
+ * unspecified), rec_offsets device uint64[num_seqs + 1]; *num_distinct (host) =
+ * rec_offsets[num_seqs].  If capacity < *num_distinct nothing is written except
+ * rec_offsets and KMC_ERR_CAPACITY is returned (valid windows, <= data bytes,
+ * always suffice).  data 16-byte aligned with data[p] = byte p of the global
+ * offsets in `indices` (device int64[num_seqs + 1]).  Synchronous on `stream`
+ * (the distinct total is returned to the host); table memory is library-owned,
+ * about 17 bytes per window. */
+#define KMC_CANON_MAX_K 31
+#define KMC_CANON_SOFTMASK 1u
+#define KMC_CANON_FORWARD 2u
+int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k, unsigned flags,
+                             uint64_t *keys, uint32_t *counts, uint64_t capacity, uint64_t *rec_offsets,
+                             uint64_t *num_distinct, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Tracing (the reference times step 1 with cudaEvents, main.cu:262-300): when set,

@@ -189,3 +189,65 @@ void oracle_min_kmeres2_row(const int32_t *sum, const int32_t *indexes, int n, i
         out[tri_idx(cur + 1, j - cur, n)] = s;
     }
 }
+
+/*
+ * Canonical k-mer counting (kmc_count_canonical_hash, include/kmc.h), k <= 31.
+ * NO REFERENCE COUNTERPART (SURVEY.md §8(c) "k=31 canonical: parity unpinned"):
+ * this is a self-oracle written from the definition, scalar and independent of
+ * the GPU algorithm (sort + run-length instead of hashing).  Windows and validity
+ * as oracle_count_record_cpu; key = MSB-first 2-bit code (first base most
+ * significant), min'ed with the reverse complement's key unless `forward`.
+ * Per record the distinct keys come out sorted ascending with their counts;
+ * rec_off[s] .. rec_off[s+1] indexes them.  Returns the distinct total.
+ */
+static int cmp_u64(const void *a, const void *b) {
+    uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+static int canon_base_code(uint8_t c, int soft) {
+    if (soft && c >= 'a' && c <= 'z') c = (uint8_t)(c - 32);
+    switch (c) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        default: return -1;
+    }
+}
+
+int64_t oracle_count_canonical(const uint8_t *data, const int64_t *indices, int64_t n, int k, int soft, int forward,
+                               uint64_t *keys, uint32_t *counts, uint64_t *rec_off) {
+    int64_t total = 0;
+    rec_off[0] = 0;
+    for (int64_t s = 0; s < n; ++s) {
+        const int64_t a = indices[s], E = indices[s + 1] - indices[s];
+        const int64_t W = E - k > 0 ? E - k : 0;
+        uint64_t *tmp = (uint64_t *)malloc((size_t)(W > 0 ? W : 1) * sizeof(uint64_t));
+        int64_t m = 0;
+        for (int64_t i = 0; i < W; ++i) {
+            uint64_t fw = 0, rc = 0;
+            int ok = 1;
+            for (int q = 0; q < k; ++q) {
+                int c = canon_base_code(data[a + i + q], soft);
+                if (c < 0) { ok = 0; break; }
+                fw = (fw << 2) | (uint64_t)c;                       /* first base most significant */
+                rc |= (uint64_t)(3 - c) << (2 * q);                 /* complement, reversed */
+            }
+            if (!ok) continue;
+            tmp[m++] = (forward || fw < rc) ? fw : rc;
+        }
+        qsort(tmp, (size_t)m, sizeof(uint64_t), cmp_u64);
+        for (int64_t i = 0; i < m;) {
+            int64_t j = i;
+            while (j < m && tmp[j] == tmp[i]) ++j;
+            keys[total] = tmp[i];
+            counts[total] = (uint32_t)(j - i);
+            ++total;
+            i = j;
+        }
+        free(tmp);
+        rec_off[s + 1] = (uint64_t)total;
+    }
+    return total;
+}

@@ -47,6 +47,8 @@ def lib():
         L.oracle_window_code.argtypes = [ctypes.c_char_p, ctypes.c_int]
         L.oracle_window_code.restype = _I64
         L.oracle_pair_distances.argtypes = [_P, _P, _I64, ctypes.c_int, _P]
+        L.oracle_count_canonical.restype = _I64
+        L.oracle_count_canonical.argtypes = [_P, _P, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.oracle_min_kmeres2_row.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
         _lib = L
     return _lib
@@ -79,6 +81,22 @@ def pair_distances(sum_, lens, k):
     out = np.zeros(max(n * (n - 1) // 2, 1), dtype=np.float32)
     lib().oracle_pair_distances(_ptr(sum_), _ptr(lens), n, k, _ptr(out))
     return out[: n * (n - 1) // 2]
+
+
+def count_canonical(data, indices, k, soft=False, forward=False):
+    """Self-oracle of kmc_count_canonical_hash: (keys u64, counts u32, rec_off u64),
+    keys sorted ascending within each record."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    indices = np.ascontiguousarray(indices, dtype=np.int64)
+    n = indices.size - 1
+    cap = max(int(indices[-1] - indices[0]) if n > 0 else 0, 1)
+    keys = np.zeros(cap, dtype=np.uint64)
+    counts = np.zeros(cap, dtype=np.uint32)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    dptr = _ptr(data) if data.size else None
+    tot = lib().oracle_count_canonical(dptr, _ptr(indices), n, k, int(soft), int(forward),
+                                       _ptr(keys), _ptr(counts), _ptr(off))
+    return keys[:tot], counts[:tot], off
 
 
 def min_kmeres2_row(sum_, indexes, cur, k, out=None):

@@ -1,0 +1,146 @@
+"""GPU parity of kmc_count_canonical_hash (k <= 31) against the canonical
+self-oracle (oracle_count_canonical: scalar, sort + run-length).
+
+No reference counterpart exists for canonical counting ("parity unpinned",
+SURVEY.md §8(c)); the self-oracle is itself pinned to the reference's dense
+counts for k <= 13 (tests/test_oracle.py), and the KMC_CANON_FORWARD mode is
+checked here against the GPU dense path on the golden fixtures.  Bit-exact
+(key, count) sets per record.
+"""
+import numpy as np
+import pytest
+
+import golden_util as G
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).to(cuda)
+
+
+def gpu_canon(kmc, cuda, data, idx, k, flags=0):
+    import torch
+    d = dev(data if data.size else np.zeros(16, np.uint8), cuda)
+    keys, counts, off = kmc.count_canonical(d, dev(idx, cuda), k, flags=flags, capacity=max(data.size, 1))
+    torch.cuda.synchronize()
+    return keys.cpu().numpy().view(np.uint64), counts.cpu().numpy().view(np.uint32), off.cpu().numpy()
+
+
+def per_record_sorted(keys, counts, off):
+    out = []
+    for s in range(off.size - 1):
+        a, b = int(off[s]), int(off[s + 1])
+        o = np.argsort(keys[a:b], kind="stable")
+        out.append((keys[a:b][o], counts[a:b][o]))
+    return out
+
+
+def assert_same(got, exp, msg=""):
+    g = per_record_sorted(*got)
+    e = per_record_sorted(*exp)
+    assert len(g) == len(e), msg
+    for s, ((gk, gc), (ek, ec)) in enumerate(zip(g, e)):
+        np.testing.assert_array_equal(gk, ek, err_msg="%s record %d keys" % (msg, s))
+        np.testing.assert_array_equal(gc, ec, err_msg="%s record %d counts" % (msg, s))
+
+
+def random_records(rng, lens, alphabet=b"ACGTN", p=(.2475, .2475, .2475, .2475, .01)):
+    recs = [np.append(rng.choice(np.frombuffer(alphabet, dtype=np.uint8), size=int(L), p=p), np.uint8(0))
+            for L in lens]
+    data = np.concatenate(recs) if recs else np.zeros(0, np.uint8)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    return data, idx
+
+
+@pytest.mark.parametrize("name,dialect", G.cases())
+def test_canonical_golden(kmc, oracle, cuda, name, dialect):
+    g = G.load(name, dialect)
+    idx = G.full_indices(g)
+    for k in (1, 3, 5, 12, 21, 31):
+        for flags in (0, kmc.CANON_SOFTMASK, kmc.CANON_FORWARD):
+            got = gpu_canon(kmc, cuda, g["data"], idx, k, flags)
+            exp = oracle.count_canonical(g["data"], idx, k, soft=bool(flags & 1), forward=bool(flags & 2))
+            assert_same(got, exp, "%s/%s k=%d flags=%d" % (name, dialect, k, flags))
+
+
+@pytest.mark.parametrize("k", [2, 7, 8, 13])
+def test_forward_mode_equals_dense_path(kmc, cuda, k):
+    """KMC_CANON_FORWARD keys are the dense bins (MSB-first instead of LE)."""
+    import torch
+    rng = np.random.default_rng(k)
+    data, idx = random_records(rng, [0, 5, 3000, 20011, 1])
+    keys, counts, off = gpu_canon(kmc, cuda, data, idx, k, kmc.CANON_FORWARD)
+    d = dev(data, cuda)
+    dense, _ = kmc.count_dense(d, dev(idx, cuda), k)
+    torch.cuda.synchronize()
+    dense = dense.cpu().numpy()
+    rebuilt = np.zeros_like(dense)
+    for s in range(idx.size - 1):
+        a, b = int(off[s]), int(off[s + 1])
+        kk = keys[a:b].astype(np.uint64)
+        le = np.zeros(kk.size, dtype=np.uint64)
+        for q in range(k):  # MSB-first -> LE code
+            le |= ((kk >> np.uint64(2 * (k - 1 - q))) & np.uint64(3)) << np.uint64(2 * q)
+        rebuilt[le.astype(np.int64), s] = counts[a:b]
+    np.testing.assert_array_equal(rebuilt, dense)
+
+
+@pytest.mark.parametrize("k", [11, 25, 31])
+def test_canonical_random_vs_oracle(kmc, oracle, cuda, k):
+    """Ragged records (empty, shorter than k, tiny, long), N runs, lowercase."""
+    rng = np.random.default_rng(100 + k)
+    lens = [0, 1, k - 1, k, k + 1, 2, 3, 40, 100_000, 7, 333_333, 0, 16, 17, 31, 32, 33]
+    data, idx = random_records(rng, lens, b"ACGTNacgt", (.2, .2, .2, .2, .04, .04, .04, .04, .04))
+    for flags in (0, kmc.CANON_SOFTMASK):
+        got = gpu_canon(kmc, cuda, data, idx, k, flags)
+        exp = oracle.count_canonical(data, idx, k, soft=bool(flags & 1))
+        assert_same(got, exp, "k=%d flags=%d" % (k, flags))
+
+
+def test_canonical_repetitive_and_many_records(kmc, oracle, cuda):
+    """Low-complexity sequence (hot keys, long probe chains) and 20 000 short records."""
+    rng = np.random.default_rng(9)
+    rep = np.frombuffer((b"A" * 5000 + b"AC" * 3000 + b"ACGTTGCA" * 2000 + b"T" * 777), dtype=np.uint8)
+    short = [np.append(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=int(L)), np.uint8(0))
+             for L in rng.integers(0, 60, size=20_000)]
+    recs = [np.append(rep, np.uint8(0))] + short
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    for k in (4, 21, 31):
+        assert_same(gpu_canon(kmc, cuda, data, idx, k), oracle.count_canonical(data, idx, k), "k=%d" % k)
+
+
+def test_canonical_size_independent_properties(kmc, cuda):
+    """64 Mbase: counts sum to the valid windows; canonical == forward folded by revcomp."""
+    import torch
+    L = 64 << 20
+    n = 4
+    data = torch.empty(n * (L + 1), dtype=torch.uint8, device=cuda)
+    kmc.synth_fill(data, n, L, 0x5EED001F)
+    idx = dev(kmc.synth_indices(n, L), cuda)
+    keys, counts, off = kmc.count_canonical(data, idx, 31)
+    torch.cuda.synchronize()
+    off = off.cpu().numpy()
+    per = [int(counts[int(off[s]):int(off[s + 1])].to(torch.int64).sum()) for s in range(n)]
+    assert per == [L - 31 + 1] * n
+    # canonical keys are <= their reverse complement's key
+    k = 31
+    kk = keys.cpu().numpy().view(np.uint64)
+    rc = np.zeros_like(kk)
+    for q in range(k):
+        rc |= (np.uint64(3) - ((kk >> np.uint64(2 * q)) & np.uint64(3))) << np.uint64(2 * (k - 1 - q))
+    assert np.all(kk <= rc)
+
+
+def test_canonical_capacity_error(kmc, cuda):
+    import torch
+    rng = np.random.default_rng(1)
+    data, idx = random_records(rng, [5000])
+    d = dev(data, cuda)
+    with pytest.raises(kmc.KmcError) as ei:
+        kmc.count_canonical(d, dev(idx, cuda), 21, capacity=10)
+    assert ei.value.code == 1009
+    with pytest.raises(kmc.KmcError):
+        kmc.count_canonical(d, dev(idx, cuda), 32)

@@ -130,3 +130,90 @@ def test_oracle_distances_match_reference_live(oracle, tmp_path):
         counts, _ = oracle.count_dense(data, idx, k)
         got = oracle.pair_distances(counts, np.diff(idx) - 1, k)
         np.testing.assert_array_equal(got, oracle.ref_seq_distances(str(fa), k))
+
+
+# ---------------------------------------------------------------------------
+# canonical k-mer self-oracle (no reference counterpart), pinned where the
+# reference reaches: for k <= 13 its counts fold from the reference's dense ones
+# ---------------------------------------------------------------------------
+def le_to_msb(code, k):
+    out = 0
+    for q in range(k):
+        out = (out << 2) | ((code >> (2 * q)) & 3)
+    return out
+
+
+def fold_dense(dense, k, forward):
+    """{(record, key): count} from a (4^k, n) dense LE histogram."""
+    mask = (1 << (2 * k)) - 1
+    res = {}
+    codes, recs = np.nonzero(dense)
+    for c, s in zip(codes.tolist(), recs.tolist()):
+        fw = le_to_msb(c, k)
+        key = fw if forward else min(fw, c ^ mask)  # LE code complemented = MSB key of the reverse complement
+        res[(s, key)] = res.get((s, key), 0) + int(dense[c, s])
+    return res
+
+
+def canon_dict(keys, counts, off):
+    res = {}
+    for s in range(off.size - 1):
+        for i in range(int(off[s]), int(off[s + 1])):
+            res[(s, int(keys[i]))] = int(counts[i])
+    return res
+
+
+@pytest.mark.parametrize("name,dialect", [("basic", "blank"), ("random", "nonl"), ("maxseqs", "blank"),
+                                          ("odd", "nonl"), ("crlf", "blank")])
+@pytest.mark.parametrize("forward", [False, True])
+def test_canonical_oracle_folds_golden_dense(oracle, name, dialect, forward):
+    g = G.load(name, dialect)
+    idx = G.full_indices(g)
+    for k in g["ks"]:
+        k = int(k)
+        exp, _ = G.dense_expected(g, k)
+        keys, counts, off = oracle.count_canonical(g["data"], idx, k, forward=forward)
+        assert canon_dict(keys, counts, off) == fold_dense(exp, k, forward), "%s k=%d" % (name, k)
+        for s in range(idx.size - 1):  # sorted, distinct within each record
+            seg = keys[int(off[s]):int(off[s + 1])]
+            assert np.all(seg[1:] > seg[:-1])
+
+
+def py_canonical(rec, k, soft=False):
+    comp = {"A": "T", "C": "G", "G": "C", "T": "A"}
+    enc = {"A": 0, "C": 1, "G": 2, "T": 3}
+    res = {}
+    txt = rec.decode("latin-1")
+    for i in range(max(0, len(txt) - k)):  # len includes the terminator
+        w = txt[i:i + k]
+        if soft:
+            w = "".join(ch.upper() if ch in "acgt" else ch for ch in w)
+        if any(ch not in enc for ch in w):
+            continue
+        rc = "".join(comp[ch] for ch in reversed(w))
+        key = min(w, rc)
+        v = 0
+        for ch in key:
+            v = (v << 2) | enc[ch]
+        res[v] = res.get(v, 0) + 1
+    return res
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 16, 17, 31])
+def test_canonical_oracle_matches_python_strings(oracle, k):
+    rng = np.random.default_rng(k)
+    recs = []
+    for L in (0, 1, k - 1, k, k + 1, 200, 777):
+        s = rng.choice(np.frombuffer(b"ACGTNacgt", dtype=np.uint8), size=max(L, 0),
+                       p=[.22, .22, .22, .22, .02, .025, .025, .025, .025])
+        recs.append(np.append(s, np.uint8(0)))
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    for soft in (False, True):
+        keys, counts, off = oracle.count_canonical(data, idx, k, soft=soft)
+        got = canon_dict(keys, counts, off)
+        exp = {}
+        for s in range(len(recs)):
+            for key, c in py_canonical(bytes(recs[s]), k, soft).items():
+                exp[(s, key)] = c
+        assert got == exp
