@@ -31,8 +31,10 @@
 namespace kmc {
 namespace {
 
-constexpr int kLowBits = 15;  // bins per bucket: 2^15 x 32-bit = 128 KB of LDS
-constexpr int kBucketBins = 1 << kLowBits;
+// Low code bits resolved by the per-list LDS histogram (2^low x 32-bit, at most
+// 128 KB); the rest select the bucket.  At least 64 buckets per record, so the
+// bucket counters of R1/R3 see few same-address LDS atomics.
+__host__ __device__ constexpr int low_bits(int k) { return 2 * k - 6 < 15 ? 2 * k - 6 : 15; }
 
 struct RParams {
     const char *data;
@@ -42,6 +44,7 @@ struct RParams {
     int derive;
     int G;           // workgroups of R1/R3
     int nbk;         // buckets per record
+    int b_lo, b_hi;  // R3: buckets scattered by this launch
     uint32_t *cnt;   // [n][nbk][G]
     uint64_t *off;   // [n*nbk*G + 1] exclusive prefix of cnt
     uint16_t *ent;   // entries
@@ -53,6 +56,7 @@ struct RParams {
 
 template <int K>
 struct RCountOp {
+    static constexpr int LOW = low_bits(K);
     uint32_t *c;  // LDS bucket counters
     __device__ void before_tile() {}
     template <bool MASKED>
@@ -61,40 +65,138 @@ struct RCountOp {
         for (int j = 0; j < 16; ++j) {
             const uint32_t code = window_code_rt<K>(lo, hi, j);
             if (!MASKED || ((W >> j) & 1u))
-                __hip_atomic_fetch_add(&c[code >> kLowBits], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&c[code >> LOW], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __device__ void after_iter(int64_t, int64_t, bool) {}
 };
 
-template <int K>
-struct RScatterOp {
-    unsigned long long *cur;  // LDS cursors: global position of the next entry per bucket
+// R3 op.  Scattering every window straight to its list costs one L2 write
+// request per 2-byte entry (64 per wave store); instead each round of one tile
+// per wave is staged in LDS, counting-sorted by bucket, and written out so that
+// consecutive lanes store consecutive entries of one list.
+//   buf  [NW][1024]  the round's codes, wave w in its own 1024-entry region
+//   srt  [NW*1024]   the round sorted by bucket
+//   off  [NBK + 1]   bucket counts -> exclusive offsets within srt
+//   gcur [NBK]       global position of each list's next entry (this workgroup)
+// Only buckets [b_lo, b_lo + b_n) are scattered (bucket-group launches).
+template <int K, int NW>
+struct RStageOp {
+    static constexpr int LOW = low_bits(K);
+    static constexpr int NBK = 1 << (2 * K - LOW);
+    static constexpr int BATCH = NW * 1024;
+    uint32_t *buf, *srt, *off, *nw;
+    unsigned long long *gcur;
     uint16_t *ent;
+    uint32_t b_lo, b_n;
+    int wave, lane, tid;
+    uint32_t fill;  // entries of this wave in the current round (wave-uniform)
+
     __device__ void before_tile() {}
+
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
+        uint32_t *dst = buf + wave * 1024;
+        uint32_t run = 0;
+        const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const uint32_t code = window_code_rt<K>(lo, hi, j);
-            if (!MASKED || ((W >> j) & 1u)) {
-                const unsigned long long pos = __hip_atomic_fetch_add(
-                    &cur[code >> kLowBits], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                ent[pos] = (uint16_t)(code & (kBucketBins - 1));
+            const bool v = (!MASKED || ((W >> j) & 1u)) && ((code >> LOW) - b_lo) < b_n;
+            const uint64_t m = __ballot(v);
+            if (v) dst[run + __popcll(m & lt)] = code;
+            run += __popcll(m);
+        }
+        fill = run;
+    }
+
+    __device__ void after_iter(int64_t, int64_t, bool active) {
+        if (lane == 0) nw[wave] = active ? fill : 0u;
+        fill = 0;
+        lds_barrier();
+        // 1. rank of every staged entry within its bucket
+        const uint32_t mine = nw[wave];
+        uint32_t code[16], rank[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t e = (uint32_t)(j * 64 + lane);
+            code[j] = e < mine ? buf[wave * 1024 + e] : 0xFFFFFFFFu;
+            if (e < mine)
+                rank[j] = __hip_atomic_fetch_add(&off[(code[j] >> LOW) - b_lo], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        lds_barrier();
+        // 2. exclusive scan of the bucket counts (off[b_n] = round total)
+        block_scan_inplace(off, (int)b_n);
+        // 3. counting-sort the round into srt
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (code[j] != 0xFFFFFFFFu) srt[off[(code[j] >> LOW) - b_lo] + rank[j]] = code[j];
+        lds_barrier();
+        // 4. coalesced write-out: srt[i] is entry (i - off[b]) of bucket b's run
+        const uint32_t total = off[b_n];
+        for (uint32_t i = tid; i < total; i += NW * 64) {
+            const uint32_t c = srt[i];
+            const uint32_t b = (c >> LOW) - b_lo;
+            ent[gcur[b] + (i - off[b])] = (uint16_t)(c & ((1u << LOW) - 1));
+        }
+        lds_barrier();
+        // 5. advance the cursors, clear the counts
+        for (uint32_t b = tid; b < b_n; b += NW * 64) {
+            gcur[b] += off[b + 1] - off[b];
+        }
+        lds_barrier();
+        for (uint32_t b = tid; b <= b_n; b += NW * 64) off[b] = 0u;
+        lds_barrier();
+    }
+
+    // in-place exclusive scan of a[0..m) with a[m] = total; all NW*64 threads
+    __device__ __forceinline__ void block_scan_inplace(uint32_t *a, int m) {
+        constexpr int T = NW * 64;
+        const int per = (m + T - 1) / T;  // consecutive elements per thread
+        const int beg = tid * per;
+        uint32_t loc = 0;
+        for (int q = 0; q < per; ++q)
+            if (beg + q < m) loc += a[beg + q];
+        // wave inclusive scan of loc
+        uint32_t x = loc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) nw[NW + wave] = x;  // wave totals after the per-wave counts
+        lds_barrier();
+        uint32_t wbase = 0;
+        for (int w2 = 0; w2 < wave; ++w2) wbase += nw[NW + w2];
+        uint32_t run = wbase + x - loc;
+        lds_barrier();  // everyone has read its inputs before they are overwritten
+        for (int q = 0; q < per; ++q) {
+            if (beg + q < m) {
+                const uint32_t v = a[beg + q];
+                a[beg + q] = run;
+                run += v;
             }
         }
+        if (tid == T - 1) a[m] = run;
+        lds_barrier();
     }
-    __device__ void after_iter(int64_t, int64_t, bool) {}
 };
 
-// R1 and R3: the piece walk of the dense kernel; SCATTER selects the op.
+// R1 and R3: the piece walk of the dense kernel; SCATTER selects the op.  The
+// scatter variant needs the whole 160 KB LDS (one workgroup per CU).
 template <int K, class Idx, bool SCATTER, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
     constexpr int NWAVES = BLOCK / 64;
-    constexpr int NBK = 1 << (2 * K - kLowBits);
+    constexpr int NBK = 1 << (2 * K - low_bits(K));
     __shared__ __attribute__((aligned(16))) unsigned long long lds64[NBK];
     __shared__ int64_t s_first;
     uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds64);
+    constexpr int SB = SCATTER ? NWAVES * 1024 : 1;
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[SB];
+    __shared__ __attribute__((aligned(16))) uint32_t s_srt[SB];
+    __shared__ uint32_t s_off[SCATTER ? NBK + 1 : 1];
+    __shared__ uint32_t s_nw[2 * NWAVES];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -116,9 +218,14 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
         if (ps >= pe) continue;
         const int64_t lbase = (s * NBK) * p.G + w;  // cnt/off index of (s, b=0, w); stride G per bucket
         for (int b = tid; b < NBK; b += BLOCK) {
-            if (SCATTER) lds64[b] = p.off[lbase + (int64_t)b * p.G];
-            else lds32[b] = 0u;
+            if (SCATTER) {
+                if (b >= p.b_lo && b < p.b_hi) lds64[b - p.b_lo] = p.off[lbase + (int64_t)b * p.G];
+            } else {
+                lds32[b] = 0u;
+            }
         }
+        if (SCATTER)
+            for (int b = tid; b <= NBK; b += BLOCK) s_off[b] = 0u;
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
         const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
@@ -126,7 +233,8 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         if constexpr (SCATTER) {
-            RScatterOp<K> op{lds64, p.ent};
+            RStageOp<K, NWAVES> op{s_buf, s_srt, s_off, s_nw, lds64, p.ent, (uint32_t)p.b_lo,
+                                   (uint32_t)(p.b_hi - p.b_lo), wave, lane, tid, 0u};
             stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         } else {
             RCountOp<K> op{lds32};
@@ -214,7 +322,9 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t *
 }
 
 // R4: one workgroup per list (s, b).
+template <int LOW>
 __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbins) {
+    constexpr int kBucketBins = 1 << LOW;
     __shared__ __attribute__((aligned(16))) uint32_t h[kBucketBins];
     const int64_t list = blockIdx.x;  // s*nbk + b
     const int64_t s = list / p.nbk, b = list % p.nbk;
@@ -283,7 +393,12 @@ __global__ __launch_bounds__(256) void radix_invalid_kernel(RParams p) {
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
-constexpr int kPassBlock = 512;
+constexpr int kPassBlock = 1024;
+// target footprint of the list lines one R3 launch keeps open (G x buckets x 128 B)
+#ifndef KMC_OPEN_LIST_MB
+#define KMC_OPEN_LIST_MB 64
+#endif
+constexpr size_t kOpenListBytes = (size_t)KMC_OPEN_LIST_MB << 20;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -294,7 +409,7 @@ struct RLayout {
 
 inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap) {
     RLayout L;
-    const int64_t nbk = (int64_t)1 << (2 * k - kLowBits);
+    const int64_t nbk = (int64_t)1 << (2 * k - low_bits(k));
     L.m = n * nbk * G;
     L.nscan = (L.m + kScanTile - 1) / kScanTile;
     size_t o = 0;
@@ -320,11 +435,7 @@ int r_grid(int device, int &G) {
     if (r_cus == 0) {
         hipError_t e = hipDeviceGetAttribute(&r_cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e != hipSuccess) return (int)e;
-        int nb = 0;
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &nb, reinterpret_cast<const void *>(&radix_pass_kernel<13, int64_t, true, kPassBlock>), kPassBlock, 0);
-        if (e != hipSuccess) return (int)e;
-        r_occ = nb > 0 ? nb : 1;
+        r_occ = 1;  // one 16-wave workgroup per CU: fewer open lists than more, smaller groups
     }
     G = r_cus * r_occ;
     return 0;
@@ -384,7 +495,9 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     p.rh = (int64_t)a->read_hi;
     p.derive = 0;
     p.G = G;
-    p.nbk = 1 << (2 * K - kLowBits);
+    p.nbk = 1 << (2 * K - low_bits(K));
+    p.b_lo = 0;
+    p.b_hi = p.nbk;
     p.cnt = reinterpret_cast<uint32_t *>(base + L.cnt);
     p.off = reinterpret_cast<uint64_t *>(base + L.off);
     p.ent = reinterpret_cast<uint16_t *>(base + L.ent);
@@ -406,8 +519,15 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kScanBlock), 0, st, bsum, L.nscan);
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)L.nscan), dim3(kScanBlock), 0, st, p.cnt, L.m, bsum,
                        p.off);
-    hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, true, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
-    hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)(n * p.nbk)), dim3(1024), 0, st, p, nbins);
+    // R3 in bucket groups whose open lines (G x buckets x 128 B) fit kOpenListBytes
+    int groups = 1;
+    while ((size_t)G * (size_t)(p.nbk / groups) * 128 > kOpenListBytes && groups < p.nbk) groups *= 2;
+    for (int gi = 0; gi < groups; ++gi) {
+        p.b_lo = gi * (p.nbk / groups);
+        p.b_hi = p.b_lo + p.nbk / groups;
+        hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, true, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
+    }
+    hipLaunchKernelGGL((radix_hist_kernel<low_bits(K)>), dim3((unsigned)(n * p.nbk)), dim3(1024), 0, st, p, nbins);
     hipLaunchKernelGGL(radix_place_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st, p, nbins);
     if (t_trace_after) {
         he = hipEventRecord(t_trace_after, st);
