@@ -28,6 +28,12 @@
 #include "kmc_internal.h"
 #include "kmc_stream.h"
 
+// Diagnostic builds only (scripts/kbench.py timing): 1 = no list stores, 2 = also
+// non-returning bucket counts, 3 = staging without the flush.  Results are wrong.
+#ifndef KMC_RSCAT_ABL
+#define KMC_RSCAT_ABL 0
+#endif
+
 namespace kmc {
 namespace {
 
@@ -76,9 +82,11 @@ struct RCountOp {
 // per wave is staged in LDS, counting-sorted by bucket, and written out so that
 // consecutive lanes store consecutive entries of one list.
 //   buf  [NW][1024]  the round's codes, wave w in its own 1024-entry region
-//   srt  [NW*1024]   the round sorted by bucket
+//   srt  [NW*1024]   the round sorted by bucket (aliases buf: buf is read into
+//                    registers before srt is written)
 //   off  [NBK + 1]   bucket counts -> exclusive offsets within srt
 //   gcur [NBK]       global position of each list's next entry (this workgroup)
+//   gdel [NBK]       this round: global position of srt index 0 of each bucket's run
 // Only buckets [b_lo, b_lo + b_n) are scattered (bucket-group launches).
 template <int K, int NW>
 struct RStageOp {
@@ -87,6 +95,7 @@ struct RStageOp {
     static constexpr int BATCH = NW * 1024;
     uint32_t *buf, *srt, *off, *nw;
     unsigned long long *gcur;
+    long long *gdel;
     uint16_t *ent;
     uint32_t b_lo, b_n;
     int wave, lane, tid;
@@ -114,6 +123,9 @@ struct RStageOp {
         if (lane == 0) nw[wave] = active ? fill : 0u;
         fill = 0;
         lds_barrier();
+#if KMC_RSCAT_ABL == 3
+        return;  // diagnostic: staging only
+#endif
         // 1. rank of every staged entry within its bucket
         const uint32_t mine = nw[wave];
         uint32_t code[16], rank[16];
@@ -121,33 +133,52 @@ struct RStageOp {
         for (int j = 0; j < 16; ++j) {
             const uint32_t e = (uint32_t)(j * 64 + lane);
             code[j] = e < mine ? buf[wave * 1024 + e] : 0xFFFFFFFFu;
+#if KMC_RSCAT_ABL == 2
+            rank[j] = 0;
+            if (e < mine) __hip_atomic_fetch_add(&off[(code[j] >> LOW) - b_lo], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
             if (e < mine)
                 rank[j] = __hip_atomic_fetch_add(&off[(code[j] >> LOW) - b_lo], 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
         }
         lds_barrier();
         // 2. exclusive scan of the bucket counts (off[b_n] = round total)
         block_scan_inplace(off, (int)b_n);
-        // 3. counting-sort the round into srt
+        // 3. counting-sort the round into srt; per bucket, the global position of
+        //    srt index 0 (gdel = cursor - offset) and the advanced cursor
 #pragma unroll
         for (int j = 0; j < 16; ++j)
             if (code[j] != 0xFFFFFFFFu) srt[off[(code[j] >> LOW) - b_lo] + rank[j]] = code[j];
-        lds_barrier();
-        // 4. coalesced write-out: srt[i] is entry (i - off[b]) of bucket b's run
-        const uint32_t total = off[b_n];
-        for (uint32_t i = tid; i < total; i += NW * 64) {
-            const uint32_t c = srt[i];
-            const uint32_t b = (c >> LOW) - b_lo;
-            ent[gcur[b] + (i - off[b])] = (uint16_t)(c & ((1u << LOW) - 1));
-        }
-        lds_barrier();
-        // 5. advance the cursors, clear the counts
         for (uint32_t b = tid; b < b_n; b += NW * 64) {
-            gcur[b] += off[b + 1] - off[b];
+            const uint32_t o0 = off[b], o1 = off[b + 1];
+            const unsigned long long g = gcur[b];
+            gdel[b] = (long long)g - (long long)o0;
+            gcur[b] = g + (o1 - o0);
         }
+        const uint32_t total = off[b_n];
         lds_barrier();
+        // 4. coalesced write-out: srt[i] is entry i + gdel[b] of bucket b's list; the
+        //    counts are cleared for the next round (nothing reads them until then)
         for (uint32_t b = tid; b <= b_n; b += NW * 64) off[b] = 0u;
-        lds_barrier();
+        uint32_t c[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t i = tid + q * NW * 64;
+            c[q] = i < total ? srt[i] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if (c[q] == 0xFFFFFFFFu) continue;
+            const uint32_t i = tid + q * NW * 64;
+            const long long pos = gdel[(c[q] >> LOW) - b_lo] + (long long)i;
+#if KMC_RSCAT_ABL >= 1
+            if (c[q] == 0xFFFFFFFEu)  // diagnostic: never true, keeps the loads
+#endif
+            ent[pos] = (uint16_t)(c[q] & ((1u << LOW) - 1));
+        }
+        lds_barrier();  // srt aliases buf: the next round's staging starts after every read
     }
 
     // in-place exclusive scan of a[0..m) with a[m] = total; all NW*64 threads
@@ -194,8 +225,8 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
     uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds64);
     constexpr int SB = SCATTER ? NWAVES * 1024 : 1;
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[SB];
-    __shared__ __attribute__((aligned(16))) uint32_t s_srt[SB];
     __shared__ uint32_t s_off[SCATTER ? NBK + 1 : 1];
+    __shared__ long long s_gdel[SCATTER ? NBK : 1];
     __shared__ uint32_t s_nw[2 * NWAVES];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -233,7 +264,7 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         if constexpr (SCATTER) {
-            RStageOp<K, NWAVES> op{s_buf, s_srt, s_off, s_nw, lds64, p.ent, (uint32_t)p.b_lo,
+            RStageOp<K, NWAVES> op{s_buf, s_buf, s_off, s_nw, lds64, s_gdel, p.ent, (uint32_t)p.b_lo,
                                    (uint32_t)(p.b_hi - p.b_lo), wave, lane, tid, 0u};
             stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         } else {
