@@ -204,83 +204,187 @@ __device__ __forceinline__ int64_t first_record_at(const P &p, int64_t pos) {
     return lo;
 }
 
+// Prefetch form of load_lane, as a raw buffer load.  The resource covers the
+// 16-byte blocks that hold readable bytes, [rl & ~15, (rh + 15) & ~15) (rebased
+// at base_off as the wave moves: the range is capped at 2^31 bytes), and the
+// hardware range check returns zeros for every lane whose block lies outside
+// it (offsets below base_off wrap to huge unsigned values).  So the prefetch is
+// one unconditional buffer_load_dwordx4 per lane and tile; in the (at most two)
+// tiles holding rl or rh inside a block, mask_range then zeroes the bytes
+// outside [rl, rh) in registers.  The blocks at rl and rh never cross a page.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const char *data, int64_t base_off, int64_t rh) {
+    const int64_t rh16 = (rh + 15) & ~(int64_t)15;
+    int64_t nrec = rh16 - base_off;
+    nrec = nrec < 0 ? 0 : (nrec > (1ll << 31) ? (1ll << 31) : nrec);
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(data) + base_off, (short)0, (int)nrec,
+                                             0x00020000);
+}
+
+// base of the resource for tiles from t on
+__device__ __forceinline__ int64_t tile_base(int64_t t, int64_t rl) {
+    const int64_t b = t << kTileShift, rl16 = rl & ~(int64_t)15;
+    return b > rl16 ? b : rl16;
+}
+
+__device__ __forceinline__ uint4 load_tile_fast(__amdgpu_buffer_rsrc_t rsrc, int64_t base_off, int64_t t,
+                                                int lane) {
+    const int64_t off = (t << kTileShift) - base_off + (int64_t)lane * 16;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(uint32_t)off, 0, KMC_NT ? 2 : 0);
+    return make_uint4(x[0], x[1], x[2], x[3]);
+}
+
+// rl or rh lies strictly inside a 16-byte block of tile t (scalar test)
+__device__ __forceinline__ bool tile_straddles(int64_t t, int64_t rl, int64_t rh) {
+    const int64_t b = t << kTileShift;
+    return ((rl & 15) != 0 && rl > b && rl < b + kTile) || ((rh & 15) != 0 && rh > b && rh < b + kTile);
+}
+
+// zero the bytes of this lane's 16 (at offset q) that lie outside [rl, rh)
+__device__ __forceinline__ uint4 mask_range(uint4 v, int64_t q, int64_t rl, int64_t rh) {
+    const int64_t lo = rl - q, hi = rh - q;
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        int64_t a = lo - 4 * d, b = hi - 4 * d;
+        a = a < 0 ? 0 : (a > 4 ? 4 : a);
+        b = b < 0 ? 0 : (b > 4 ? 4 : b);
+        uint32_t m = 0u;
+        if (b > a) {
+            const uint32_t upto = b == 4 ? 0xFFFFFFFFu : ((1u << (8 * (uint32_t)b)) - 1u);
+            m = upto & ~((1u << (8 * (uint32_t)a)) - 1u);
+        }
+        w[d] &= m;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // One wave streams tiles [t0, t1) and counts the windows that start in [ps, pe),
 // over `per` workgroup-uniform iterations (waves with fewer tiles keep calling
-// op.after_iter, so workgroup barriers inside it stay matched).  Tiles are
-// streamed KMC_PF ahead; the decode of tile t+1 doubles as lane 63's halo of t.
+// op.after_iter, so workgroup barriers inside it stay matched).  Tile t+1 is
+// decoded while tile t is counted (it is lane 63's halo of t).
+//
+// Prefetch: KMC_PF tiles ahead, in a ring of KMC_PF+1 register slots whose index
+// is a compile-time constant in every step (the loop is unrolled by the ring
+// size), issued unconditionally (load_tile_fast) so that no branch merges pending
+// and completed loads.  Both matter: register moves between slots (r[q] =
+// r[q+1]) or a load inside a branch make the compiler wait for the load it has
+// just issued (s_waitcnt vmcnt(0)) before the next decode, which leaves one tile
+// in flight per wave whatever KMC_PF says.
+template <int K>
+struct TileStream {
+    static constexpr int PF = KMC_PF;
+    static constexpr int NS = PF + 1;
+    const char *__restrict__ data;
+    int64_t t0, ps, pe, rl, rh;
+    int lane;
+    __amdgpu_buffer_rsrc_t rsrc;
+    int64_t base_off;
+    uint4 r[NS];
+    uint32_t c_cur, v_cur;
+
+    // step i (tile t0 + i < t1); S = i mod NS is the slot of tile t0 + i
+    template <int S, class Op>
+    __device__ __forceinline__ void step(int64_t i, int64_t per, Op &op) {
+        const int64_t t = t0 + i;
+        constexpr int SN = (S + 1) % NS, SL = (S + PF) % NS;
+        r[SL] = load_tile_fast(rsrc, base_off, t + PF, lane);
+        if (tile_straddles(t + 1, rl, rh))
+            r[SN] = mask_range(r[SN], ((t + 1) << kTileShift) + (int64_t)lane * 16, rl, rh);
+        const uint4 r_cur = r[S], r_nxt = r[SN];
+        uint32_t c_nxt, v_nxt;
+#if KMC_ABLATE == 2
+        c_nxt = r_nxt.x ^ r_nxt.y ^ r_nxt.z ^ r_nxt.w;
+        v_nxt = 0u;
+#else
+        decode16(r_nxt, c_nxt, v_nxt);
+#endif
+        // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
+        uint32_t hc = from_next_lane(c_cur);
+        uint32_t hv = from_next_lane(v_cur);
+        const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
+        const uint32_t v0 = __builtin_amdgcn_readlane(v_nxt, 0);
+        if (lane == 63) {
+            hc = c0;
+            hv = v0;
+        }
+        op.before_tile();
+        const int64_t base = t << kTileShift;
+        const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
+        if (interior && !__any((v_cur | hv) != 0u)) {
+#if KMC_ABLATE == 0
+            op.template tile<false>(c_cur, hc, 0xFFFFu);
+#else
+            asm volatile("" ::"v"(c_cur), "v"(hc));
+#endif
+        } else {
+            // boundary tile or invalid bytes: exact per-window mask
+            const int64_t pos = base + (int64_t)lane * 16;
+            const int64_t dlo = ps - pos, dhi = pe - pos;
+            const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
+            const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
+            const uint32_t b_own = bad_mask16(r_cur);
+            uint32_t b_next = from_next_lane(b_own);
+            const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
+            if (lane == 63) b_next = b0;
+            const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
+#if KMC_ABLATE == 0
+            op.template tile<true>(c_cur, hc, W);
+#else
+            asm volatile("" ::"v"(c_cur), "v"(hc), "v"(W));
+#endif
+        }
+        c_cur = c_nxt;
+        v_cur = v_nxt;
+        op.after_iter(i, per, true);
+    }
+
+    // steps i .. i+NS-1, stopping at n (the wave's tile count)
+    template <int S, class Op>
+    __device__ __forceinline__ void steps(int64_t i, int64_t n, int64_t per, Op &op) {
+        if constexpr (S < NS) {
+            if constexpr (S == 0) {
+                base_off = tile_base(t0 + i, rl);
+                rsrc = tile_rsrc(data, base_off, rh);
+            }
+            if (i + S < n) {
+                step<S>(i + S, per, op);
+                steps<S + 1>(i, n, per, op);
+            }
+        }
+    }
+};
+
 template <int K, class Op>
 __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
                                              int64_t ps, int64_t pe, int64_t rl, int64_t rh, int lane, Op &op) {
-    constexpr int PF = KMC_PF;  // r[0] = tile t, r[i] = tile t+i
-    uint4 r[PF + 1];
+    using TS = TileStream<K>;
+    const int64_t n = t1 > t0 ? t1 - t0 : 0;  // <= per
+    if (n > 0) {
+        TS ts;
+        ts.data = data;
+        ts.t0 = t0;
+        ts.ps = ps;
+        ts.pe = pe;
+        ts.rl = rl;
+        ts.rh = rh;
+        ts.lane = lane;
 #pragma unroll
-    for (int q = 0; q <= PF; ++q) r[q] = make_uint4(0u, 0u, 0u, 0u);
-    uint32_t c_cur = 0u, v_cur = 0u;
-    if (t0 < t1) {
+        for (int q = 0; q < TS::NS; ++q) ts.r[q] = make_uint4(0u, 0u, 0u, 0u);
+        ts.base_off = tile_base(t0, rl);
+        ts.rsrc = tile_rsrc(data, ts.base_off, rh);
 #pragma unroll
-        for (int q = 0; q < PF; ++q)
-            if (t0 + q <= t1) r[q] = load_lane(data, t0 + q, lane, rl, rh);
+        for (int q = 0; q < TS::PF; ++q) ts.r[q] = load_tile_fast(ts.rsrc, ts.base_off, t0 + q, lane);
+        if (tile_straddles(t0, rl, rh)) ts.r[0] = mask_range(ts.r[0], (t0 << kTileShift) + (int64_t)lane * 16, rl, rh);
 #if KMC_ABLATE == 2
-        c_cur = r[0].x ^ r[0].y;
+        ts.c_cur = ts.r[0].x ^ ts.r[0].y;
+        ts.v_cur = 0u;
 #else
-        decode16(r[0], c_cur, v_cur);
+        decode16(ts.r[0], ts.c_cur, ts.v_cur);
 #endif
+        for (int64_t i = 0; i < n; i += TS::NS) ts.template steps<0>(i, n, per, op);
     }
-    for (int64_t i = 0; i < per; ++i) {
-        const int64_t t = t0 + i;
-        if (t < t1) {
-            r[PF] = make_uint4(0u, 0u, 0u, 0u);
-            if (t + PF <= t1) r[PF] = load_lane(data, t + PF, lane, rl, rh);
-            const uint4 r_cur = r[0], r_nxt = r[1];
-            uint32_t c_nxt, v_nxt;
-#if KMC_ABLATE == 2
-            c_nxt = r_nxt.x ^ r_nxt.y ^ r_nxt.z ^ r_nxt.w;
-            v_nxt = 0u;
-#else
-            decode16(r_nxt, c_nxt, v_nxt);
-#endif
-            // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
-            uint32_t hc = from_next_lane(c_cur);
-            uint32_t hv = from_next_lane(v_cur);
-            const uint32_t c0 = __builtin_amdgcn_readlane(c_nxt, 0);
-            const uint32_t v0 = __builtin_amdgcn_readlane(v_nxt, 0);
-            if (lane == 63) {
-                hc = c0;
-                hv = v0;
-            }
-            op.before_tile();
-            const int64_t base = t << kTileShift;
-            const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
-            if (interior && !__any((v_cur | hv) != 0u)) {
-#if KMC_ABLATE == 0
-                op.template tile<false>(c_cur, hc, 0xFFFFu);
-#else
-                asm volatile("" ::"v"(c_cur), "v"(hc));
-#endif
-            } else {
-                // boundary tile or invalid bytes: exact per-window mask
-                const int64_t pos = base + (int64_t)lane * 16;
-                const int64_t dlo = ps - pos, dhi = pe - pos;
-                const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
-                const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
-                const uint32_t b_own = bad_mask16(r_cur);
-                uint32_t b_next = from_next_lane(b_own);
-                const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
-                if (lane == 63) b_next = b0;
-                const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
-#if KMC_ABLATE == 0
-                op.template tile<true>(c_cur, hc, W);
-#else
-                asm volatile("" ::"v"(c_cur), "v"(hc), "v"(W));
-#endif
-            }
-#pragma unroll
-            for (int q = 0; q < PF; ++q) r[q] = r[q + 1];
-            c_cur = c_nxt;
-            v_cur = v_nxt;
-        }
-        op.after_iter(i, per, t < t1);
-    }
+    for (int64_t i = n; i < per; ++i) op.after_iter(i, per, false);
 }
 
 // Code of window j (bases j .. j+K-1, K <= 16) of a lane with bases lo : hi.
