@@ -8,14 +8,19 @@
 //
 // Layout in HBM: one open-addressing table segment per record, sized from the
 // record's window count (load <= 0.7), SoA slots keys[u64] / counts[u32], empty key
-// = ~0 (no k-mer reaches it: 62 bits at most).  Insert = one read of the home slot,
-// a 64-bit CAS only when it is empty, then a 32-bit add; linear probing inside the
-// record's segment.  Compaction counts each record's occupied slots, scans them on
-// the host (the call returns the distinct total, so it synchronises anyway) and
-// writes the (key, count) pairs record by record.
+// = ~0 (no k-mer reaches it: 62 bits at most).  A slot's count word holds the
+// occurrences minus one: insert = a 64-bit CAS on the home slot, which claims an
+// empty slot (the first occurrence: nothing else to do) or returns the key that
+// holds it (the same key: one 32-bit add), linear probing inside the record's
+// segment.  Compaction is a stream compaction of the slot array in slot order:
+// live slots per 4096-slot tile, an exclusive scan over tiles (kmc_scan.h), each
+// record's output offset = the live slots before its segment, then every tile
+// writes its (key, count) pairs at its offset.  Records are contiguous segments,
+// so each record's pairs come out contiguous, as the ABI requires.
 //
-// Bound: random device-scope atomics (two per k-mer, memory-side), not HBM
-// streaming; SURVEY.md §8(d) prices a k-mer at 1 B in + 16 B of table.
+// Bound: random device-scope atomics (one per k-mer when keys are distinct,
+// memory-side), not HBM streaming; SURVEY.md §8(d) prices a k-mer at 1 B in +
+// 16 B of table.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -24,6 +29,7 @@
 #include <vector>
 
 #include "kmc.h"
+#include "kmc_scan.h"
 #include "kmc_stream.h"
 
 namespace kmc {
@@ -40,10 +46,11 @@ struct HParams {
     uint32_t flags;
     const uint64_t *tbase;  // device, n + 1: table segment of record r
     unsigned long long *keys;
-    uint32_t *counts;
-    unsigned long long *occ;     // [n] occupied slots per record
-    unsigned long long *cursor;  // [n] emit cursors
-    const uint64_t *rec_off;     // [n + 1] output offsets
+    uint32_t *counts;            // occurrences - 1 of the slot's key
+    uint64_t nslots;
+    uint32_t *tile_cnt;          // [ntiles] live slots per compaction tile
+    uint64_t *tile_off;          // [ntiles + 1] exclusive scan of tile_cnt
+    uint64_t *rec_off;           // [n + 1] output offsets
     uint64_t *out_keys;
     uint32_t *out_counts;
 };
@@ -127,11 +134,8 @@ __global__ __launch_bounds__(256) void hash_insert_kernel(HParams p) {
             const uint64_t base = p.tbase[r], cap = p.tbase[r + 1] - base;
             uint64_t s = __umul64hi(fmix64(key), cap);
             for (;;) {
-                unsigned long long cur = p.keys[base + s];
-                if (cur == kEmpty) {
-                    cur = atomicCAS(&p.keys[base + s], kEmpty, (unsigned long long)key);
-                    if (cur == kEmpty) cur = key;
-                }
+                const unsigned long long cur = atomicCAS(&p.keys[base + s], kEmpty, (unsigned long long)key);
+                if (cur == kEmpty) break;  // claimed: first occurrence (count word stays 0)
                 if (cur == key) {
                     __hip_atomic_fetch_add(&p.counts[base + s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
@@ -142,55 +146,74 @@ __global__ __launch_bounds__(256) void hash_insert_kernel(HParams p) {
     }
 }
 
-__device__ __forceinline__ int64_t slot_record(const uint64_t *tbase, int64_t n, uint64_t s) {
-    int64_t a = 0, b = n;  // tbase[a] <= s < tbase[b]
-    while (b - a > 1) {
-        const int64_t m = (a + b) >> 1;
-        if (tbase[m] <= s) a = m; else b = m;
+// Stream compaction of the slot array.  A tile is kCompTile consecutive slots,
+// kScanBlock threads x 4 slots each (two uint4 key loads, one uint4 count load).
+constexpr int kCompPer = 4;
+constexpr int64_t kCompTile = (int64_t)kScanBlock * kCompPer;
+
+__device__ __forceinline__ uint32_t live4(const HParams &p, uint64_t s0, unsigned long long k[4]) {
+    uint32_t m = 0;
+    if (s0 + 4 <= p.nslots) {
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(p.keys + s0);
+        const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(p.keys + s0 + 2);
+        k[0] = a.x; k[1] = a.y; k[2] = b.x; k[3] = b.y;
+    } else {
+        for (int q = 0; q < 4; ++q) k[q] = s0 + q < p.nslots ? p.keys[s0 + q] : kEmpty;
     }
-    return a;
+    for (int q = 0; q < 4; ++q) m |= (uint32_t)(k[q] != kEmpty) << q;
+    return m;
 }
 
-// Per-record slot claims of one wave: one atomic per wave when all its live
-// slots belong to one record (the common case: segments are long), else one per
-// lane.  Returns the lane's position among the record's claims of this call.
-__device__ __forceinline__ uint64_t wave_claim(unsigned long long *ctr, bool live, int64_t r) {
+// live slots per tile
+__global__ __launch_bounds__(kScanBlock) void hash_tilecount_kernel(HParams p) {
+    __shared__ uint64_t sh[kScanBlock / 64];
+    const uint64_t s0 = (uint64_t)blockIdx.x * kCompTile + (uint64_t)threadIdx.x * kCompPer;
+    unsigned long long k[4];
+    const uint32_t m = live4(p, s0, k);
+    uint64_t total;
+    block_excl_scan((uint64_t)__popc(m), sh, total);
+    if (threadIdx.x == 0) p.tile_cnt[blockIdx.x] = (uint32_t)total;
+}
+
+// rec_off[r] = live slots before record r's segment (one wave per record; r = n: the total)
+__global__ __launch_bounds__(256) void hash_recoff_kernel(HParams p, int64_t ntiles) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const unsigned long long live_mask = __ballot(live);
-    if (!live_mask) return 0;
-    const int leader = __ffsll((long long)live_mask) - 1;
-    const int64_t rl = __shfl(r, leader);
-    const unsigned long long same = __ballot(live && r == rl);
-    if (same == live_mask) {
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(&ctr[rl], (unsigned long long)__popcll(live_mask));
-        base = __shfl(base, leader);
-        return base + __popcll(live_mask & ((1ull << lane) - 1));
+    if (r > p.n) return;
+    if (r == p.n) {
+        if (lane == 0) p.rec_off[r] = p.tile_off[ntiles];
+        return;
     }
-    return live ? atomicAdd(&ctr[r], 1ull) : 0;
+    const uint64_t pos = p.tbase[r];
+    const uint64_t t = pos / (uint64_t)kCompTile, t0 = t * (uint64_t)kCompTile;
+    uint32_t c = 0;
+    for (uint64_t s = t0 + lane; s < pos; s += 64) c += p.keys[s] != kEmpty;
+    c = wave_sum(c);
+    if (lane == 0) p.rec_off[r] = p.tile_off[t] + c;
 }
 
-// occupied slots per record
-__global__ __launch_bounds__(256) void hash_occ_kernel(HParams p, uint64_t nslots) {
-    for (uint64_t s0 = (uint64_t)blockIdx.x * 256; s0 < nslots; s0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t s = s0 + threadIdx.x;
-        const bool live = s < nslots && p.keys[s] != kEmpty;
-        const int64_t r = live ? slot_record(p.tbase, p.n, s) : 0;
-        wave_claim(p.occ, live, r);
-    }
-}
-
-// (key, count) of every occupied slot -> its record's output range
-__global__ __launch_bounds__(256) void hash_emit_kernel(HParams p, uint64_t nslots) {
-    for (uint64_t s0 = (uint64_t)blockIdx.x * 256; s0 < nslots; s0 += (uint64_t)gridDim.x * 256) {
-        const uint64_t s = s0 + threadIdx.x;
-        const unsigned long long key = s < nslots ? p.keys[s] : kEmpty;
-        const bool live = key != kEmpty;
-        const int64_t r = live ? slot_record(p.tbase, p.n, s) : 0;
-        const uint64_t o = wave_claim(p.cursor, live, r);
-        if (live) {
-            p.out_keys[p.rec_off[r] + o] = key;
-            p.out_counts[p.rec_off[r] + o] = p.counts[s];
+// (key, count) of every live slot, in slot order, at its tile's offset
+__global__ __launch_bounds__(kScanBlock) void hash_emit_kernel(HParams p) {
+    __shared__ uint64_t sh[kScanBlock / 64];
+    const uint64_t s0 = (uint64_t)blockIdx.x * kCompTile + (uint64_t)threadIdx.x * kCompPer;
+    unsigned long long k[4];
+    const uint32_t m = live4(p, s0, k);
+    uint64_t total;
+    uint64_t o = p.tile_off[blockIdx.x] + block_excl_scan((uint64_t)__popc(m), sh, total);
+    if (m) {
+        uint32_t c[4];
+        if (s0 + 4 <= p.nslots) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(p.counts + s0);
+            c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+        } else {
+            for (int q = 0; q < 4; ++q) c[q] = s0 + q < p.nslots ? p.counts[s0 + q] : 0u;
+        }
+        for (int q = 0; q < 4; ++q) {
+            if ((m >> q) & 1u) {
+                p.out_keys[o] = k[q];
+                p.out_counts[o] = c[q] + 1u;
+                ++o;
+            }
         }
     }
 }
@@ -240,13 +263,15 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
         tb[r + 1] = tb[r] + seg_cap(hidx[r + 1] - hidx[r], k);
     }
     const uint64_t nslots = tb[n];
-    // workspace: tbase, occ, cursor, rec_off, keys, counts
+    const int64_t ntiles = (int64_t)((nslots + kCompTile - 1) / kCompTile);
+    // workspace: tbase, keys, counts, tile counts, tile offsets, scan block sums
     size_t o = 0;
     const size_t o_tb = o; o += al256((n + 1) * 8);
-    const size_t o_occ = o; o += al256(n * 8);
-    const size_t o_cur = o; o += al256(n * 8);
     const size_t o_keys = o; o += al256(nslots * 8);
     const size_t o_cnt = o; o += al256(nslots * 4);
+    const size_t o_tc = o; o += al256((size_t)ntiles * 4);
+    const size_t o_to = o; o += al256((size_t)(ntiles + 1) * 8);
+    const size_t o_bs = o; o += al256((size_t)(scan_tiles(ntiles) + 1) * 8);
     const size_t total = o;
     int device = 0;
     he = hipGetDevice(&device);
@@ -274,15 +299,16 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     p.k = k;
     p.flags = flags;
     p.tbase = reinterpret_cast<uint64_t *>(ws + o_tb);
-    p.occ = reinterpret_cast<unsigned long long *>(ws + o_occ);
-    p.cursor = reinterpret_cast<unsigned long long *>(ws + o_cur);
     p.keys = reinterpret_cast<unsigned long long *>(ws + o_keys);
     p.counts = reinterpret_cast<uint32_t *>(ws + o_cnt);
+    p.nslots = nslots;
+    p.tile_cnt = reinterpret_cast<uint32_t *>(ws + o_tc);
+    p.tile_off = reinterpret_cast<uint64_t *>(ws + o_to);
+    uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + o_bs);
     p.rec_off = rec_offsets;
     p.out_keys = keys;
     p.out_counts = counts;
     if ((he = hipMemcpyAsync((void *)p.tbase, tb.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
-        (he = hipMemsetAsync(p.occ, 0, n * 8, stream)) || (he = hipMemsetAsync(p.cursor, 0, n * 8, stream)) ||
         (he = hipMemsetAsync(p.keys, 0xFF, nslots * 8, stream)) || (he = hipMemsetAsync(p.counts, 0, nslots * 4, stream)))
         return (int)he;
     const int64_t chunks = ((p.hi + 15) >> 4) - (p.lo >> 4);
@@ -290,19 +316,18 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
         const int64_t blocks = std::min<int64_t>((chunks + 255) / 256, 1 << 16);
         hipLaunchKernelGGL(hash_insert_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
     }
-    const unsigned sblocks = (unsigned)std::min<uint64_t>((nslots + 255) / 256, 1 << 16);
-    hipLaunchKernelGGL(hash_occ_kernel, dim3(sblocks), dim3(256), 0, stream, p, nslots);
-    std::vector<uint64_t> occ(n), off(n + 1);
-    if ((he = hipGetLastError()) || (he = hipMemcpyAsync(occ.data(), p.occ, n * 8, hipMemcpyDeviceToHost, stream)) ||
+    hipLaunchKernelGGL(hash_tilecount_kernel, dim3((unsigned)ntiles), dim3(kScanBlock), 0, stream, p);
+    excl_scan_u32(p.tile_cnt, ntiles, bsum, p.tile_off, stream);
+    hipLaunchKernelGGL(hash_recoff_kernel, dim3((unsigned)((n + 1 + 3) / 4)), dim3(256), 0, stream, p, ntiles);
+    uint64_t distinct = 0;
+    if ((he = hipGetLastError()) ||
+        (he = hipMemcpyAsync(&distinct, p.rec_off + n, 8, hipMemcpyDeviceToHost, stream)) ||
         (he = hipStreamSynchronize(stream)))
         return (int)he;
-    off[0] = 0;
-    for (int64_t r = 0; r < n; ++r) off[r + 1] = off[r] + occ[r];
-    *num_distinct = off[n];
-    if (off[n] > capacity) return KMC_ERR_CAPACITY;
-    if (off[n] && (!keys || !counts)) return KMC_ERR_INVALID_ARG;
-    if ((he = hipMemcpyAsync(rec_offsets, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream))) return (int)he;
-    hipLaunchKernelGGL(hash_emit_kernel, dim3(sblocks), dim3(256), 0, stream, p, nslots);
+    *num_distinct = distinct;
+    if (distinct > capacity) return KMC_ERR_CAPACITY;
+    if (distinct && (!keys || !counts)) return KMC_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(hash_emit_kernel, dim3((unsigned)ntiles), dim3(kScanBlock), 0, stream, p);
     if ((he = hipGetLastError()) || (he = hipStreamSynchronize(stream))) return (int)he;
     return KMC_OK;
 }

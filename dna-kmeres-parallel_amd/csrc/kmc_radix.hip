@@ -26,6 +26,7 @@
 
 #include "kmc.h"
 #include "kmc_internal.h"
+#include "kmc_scan.h"
 #include "kmc_stream.h"
 
 // Diagnostic builds only (scripts/kbench.py timing): 1 = no list stores, 2 = also
@@ -279,78 +280,6 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
     }
 }
 
-// R2: exclusive scan of cnt (uint32) into off (uint64), three phases.
-constexpr int kScanBlock = 1024, kScanPer = 4, kScanTile = kScanBlock * kScanPer;
-
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, uint64_t &total) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    uint64_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) sh[wid] = x;
-    __syncthreads();
-    if (wid == 0) {
-        uint64_t t = lane < kScanBlock / 64 ? sh[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t y = __shfl_up(t, o);
-            if (lane >= o) t += y;
-        }
-        if (lane < kScanBlock / 64) sh[lane] = t;
-    }
-    __syncthreads();
-    total = sh[kScanBlock / 64 - 1];
-    const uint64_t before = wid ? sh[wid - 1] : 0;
-    __syncthreads();
-    return before + x - v;
-}
-
-__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t *in, int64_t m, uint64_t *bsum) {
-    __shared__ uint64_t sh[kScanBlock / 64];
-    const int64_t base = (int64_t)blockIdx.x * kScanTile;
-    uint64_t v = 0;
-    for (int q = 0; q < kScanPer; ++q) {
-        const int64_t i = base + (int64_t)q * kScanBlock + threadIdx.x;
-        if (i < m) v += in[i];
-    }
-    uint64_t total;
-    block_excl_scan(v, sh, total);
-    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kScanBlock) void scan_blocks_kernel(uint64_t *bsum, int64_t nb) {
-    __shared__ uint64_t sh[kScanBlock / 64];
-    uint64_t carry = 0;
-    for (int64_t base = 0; base < nb; base += kScanBlock) {
-        const int64_t i = base + threadIdx.x;
-        const uint64_t v = i < nb ? bsum[i] : 0;
-        uint64_t total;
-        const uint64_t ex = block_excl_scan(v, sh, total);
-        if (i < nb) bsum[i] = carry + ex;
-        carry += total;
-    }
-}
-
-__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t *in, int64_t m, const uint64_t *bsum,
-                                                                uint64_t *out) {
-    __shared__ uint64_t sh[kScanBlock / 64];
-    const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
-    uint64_t v[kScanPer], tsum = 0;
-    for (int q = 0; q < kScanPer; ++q) {
-        v[q] = (base + q < m) ? in[base + q] : 0;
-        tsum += v[q];
-    }
-    uint64_t total;
-    uint64_t run = bsum[blockIdx.x] + block_excl_scan(tsum, sh, total);
-    for (int q = 0; q < kScanPer; ++q) {
-        if (base + q < m) out[base + q] = run;
-        run += v[q];
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) out[m] = run;  // grand total
-}
 
 // R4: one workgroup per list (s, b).
 template <int LOW>
@@ -546,10 +475,7 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     he = hipMemsetAsync(p.cnt, 0, (size_t)L.m * 4, st);
     if (he != hipSuccess) return (int)he;
     hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, false, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)L.nscan), dim3(kScanBlock), 0, st, p.cnt, L.m, bsum);
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kScanBlock), 0, st, bsum, L.nscan);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)L.nscan), dim3(kScanBlock), 0, st, p.cnt, L.m, bsum,
-                       p.off);
+    excl_scan_u32(p.cnt, L.m, bsum, p.off, st);
     // R3 in bucket groups whose open lines (G x buckets x 128 B) fit kOpenListBytes
     int groups = 1;
     while ((size_t)G * (size_t)(p.nbk / groups) * 128 > kOpenListBytes && groups < p.nbk) groups *= 2;

@@ -1,0 +1,114 @@
+#!/usr/bin/env python3
+"""Benchmark of the two non-headline BASELINE.json configurations (diagnostic;
+bench.py times configs[1], the headline):
+  C3  10 Gbase synthetic, k = 13 dense histogram (radix path), whole call timed
+  C4  GRCh38-sized synthetic (3.1 Gbase, 25 chromosome-like records, ~5 % N runs,
+      ~50 % soft-masked lowercase), k = 31 canonical counting with KMC_CANON_SOFTMASK
+Input resident in HBM; one JSON line per configuration.
+Usage: python scripts/cbench.py [--configs c3,c4] [--iters 3] [--gbases-c4 3.1]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dna-kmeres-parallel_amd"))
+
+
+def grch38_like(torch, dev, gbases, seed=38):
+    """Synthetic stand-in for GRCh38 (not in the container): chromosome-like
+    record lengths, uniform bases, N runs and lowercase runs."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    # relative sizes of chr1..22, X, Y, M-ish
+    rel = [248, 242, 198, 190, 181, 171, 159, 145, 138, 134, 135, 133, 114, 107, 102, 90, 83, 80, 59, 64, 47, 51,
+           156, 57, 1]
+    tot = sum(rel)
+    lens = [max(1000, int(gbases * 1e9 * r / tot)) for r in rel]
+    n = len(lens)
+    nbytes = sum(L + 1 for L in lens)
+    data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    chunk = 1 << 28
+    for o in range(0, nbytes, chunk):
+        m = min(chunk, nbytes - o)
+        data[o:o + m] = lut[torch.randint(0, 4, (m,), device=dev, generator=g, dtype=torch.int64).to(torch.uint8).long()]
+        # runs of 4096 bases: ~50 % lowercase, ~5 % N
+        r = torch.rand((m + 4095) // 4096, device=dev, generator=g)
+        run = r.repeat_interleave(4096)[:m]
+        seg = data[o:o + m]
+        seg[run < 0.5] += 32
+        seg[run > 0.95] = ord("N")
+    off = [0]
+    for L in lens:
+        off.append(off[-1] + L + 1)
+    offs = torch.tensor(off, dtype=torch.int64)
+    data[offs[1:] - 1] = 0
+    return data, offs.to(dev), lens
+
+
+def timed(torch, fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2], ts[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c4")
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--gbases-c3", type=float, default=10.0)
+    ap.add_argument("--gbases-c4", type=float, default=3.1)
+    ap.add_argument("--k3", type=int, default=13)
+    a = ap.parse_args()
+    import torch
+    import kmc
+    dev = torch.device("cuda:0")
+    cfgs = a.configs.split(",")
+    if "c3" in cfgs:
+        recs = 10
+        L = int(a.gbases_c3 * 1e9 / recs)
+        data = torch.empty(recs * (L + 1), dtype=torch.uint8, device=dev)
+        kmc.synth_fill(data, recs, L, 0x5EED0000 + a.k3)
+        idx = torch.from_numpy(kmc.synth_indices(recs, L)).to(dev)
+        k = a.k3
+        out = torch.empty((1 << (2 * k), recs), dtype=torch.int32, device=dev)
+        args = kmc.dense_args(data, idx, k, out)
+        ws = torch.empty(kmc.dense_ex_workspace_size(args), dtype=torch.uint8, device=dev)
+        args = kmc.dense_args(data, idx, k, out, workspace=ws)
+        med, best = timed(torch, lambda: kmc.count_dense_ex(args), a.iters)
+        kmers = recs * (L - k + 1)
+        alg = data.numel() + 4 * (1 << (2 * k)) * recs
+        print(json.dumps({"config": "C3", "k": k, "records": recs, "bases": recs * L, "s_med": med, "s_min": best,
+                          "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9,
+                          "frac8TB": alg / med / 8e12}), flush=True)
+        del data, out, ws, args
+        torch.cuda.empty_cache()
+    if "c4" in cfgs:
+        data, idx, lens = grch38_like(torch, dev, a.gbases_c4)
+        k = 31
+        kmers = sum(max(0, L - k + 1) for L in lens)
+        res = {}
+
+        def run():
+            res["r"] = kmc.count_canonical(data, idx, k, flags=kmc.CANON_SOFTMASK)
+        med, best = timed(torch, run, a.iters)
+        keys, counts, off = res["r"]
+        tot = int(counts.sum().item())
+        alg = 17 * kmers  # 1 B input + 16 B table slot per k-mer
+        print(json.dumps({"config": "C4", "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
+                          "valid_windows": tot, "distinct": int(keys.numel()), "s_med": med, "s_min": best,
+                          "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9,
+                          "frac8TB": alg / med / 8e12}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
