@@ -3,7 +3,8 @@
 // calling the HIP kernels only through the C ABI of include/kmc.h.
 //
 // Flow (the reference's, with its hard-coded constants turned into options):
-//   importSeqs / importSeqsNoNL           -> kmc_fasta_load          (main.cu:163, 474-545 / 401-473)
+//   importSeqs / importSeqsNoNL           -> kmc_fasta_load_device (file -> HBM, parsed on the GPU;
+//                                            --host-loader: kmc_fasta_load) (main.cu:163, 474-545 / 401-473)
 //   step 1: sumKmereCoincidencesGlobalMemory -> kmc_count_dense / kmc_count_multi
 //                                               (--dropin: sumKmereCoincidencesGlobalMemory_hip)
 //                                                                    (main.cu:287-300)
@@ -41,6 +42,7 @@ struct Options {
     bool softmask = false;
     bool distances = true;
     bool quiet = false;
+    bool host_loader = false;
 };
 
 void usage(FILE *f) {
@@ -62,6 +64,8 @@ void usage(FILE *f) {
             "  --canonical       canonical k-mers (k <= %d) instead of the dense histogram; with\n"
             "                    --counts writes 'record<TAB>kmer<TAB>count' lines\n"
             "  --softmask        with --canonical: lowercase acgt count as bases\n"
+            "  --host-loader     parse the FASTA on the host (kmc_fasta_load) instead of on the GPU\n"
+            "                    (kmc_fasta_load_device); --gpus > 1 always uses the host buffer\n"
             "  -q                quiet (no progress lines)\n",
             KMC_DROPIN_K, KMC_DENSE_MAX_K, KMC_CANON_MAX_K, KMC_MAX_SEQS_REFERENCE, KMC_MAX_SEQS_REFERENCE + 1,
             KMC_DROPIN_K, KMC_CANON_MAX_K);
@@ -103,6 +107,8 @@ int parse(int argc, char **argv, Options &o) {
             o.canonical = true;
         } else if (a == "--softmask") {
             o.softmask = true;
+        } else if (a == "--host-loader") {
+            o.host_loader = true;
         } else if (a == "-q") {
             o.quiet = true;
         } else if (!a.empty() && a[0] == '-') {
@@ -188,20 +194,7 @@ float ms_between(hipEvent_t a, hipEvent_t b) {
 }
 
 int run(const Options &o) {
-    kmc_fasta *fa = nullptr;
-    const auto tl0 = std::chrono::steady_clock::now();
-    KMCCHK(kmc_fasta_load(o.input.c_str(), o.dialect, o.max_seqs, &fa));
-    const auto tl1 = std::chrono::steady_clock::now();
-    const uint64_t n = kmc_fasta_num_seqs(fa);
-    const uint64_t bytes = kmc_fasta_data_bytes(fa);
-    const int64_t *hidx = kmc_fasta_indices(fa);
     const int k = o.k;
-    if (!o.quiet) {
-        printf("K = %d\n", k);
-        printf("Size all seqs:%" PRIu64 "\n", bytes);  // main.cu:166-167
-        printf("%" PRIu64 " sequences read .\n", n);
-        printf("Loader: %.1f ms\n", std::chrono::duration<double, std::milli>(tl1 - tl0).count());
-    }
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
     if (ndev < 1) return fprintf(stderr, "kmc: no HIP device\n"), 1;
@@ -212,17 +205,38 @@ int run(const Options &o) {
     hipEvent_t ev[6];
     for (auto &e : ev) HIPCHK(hipEventCreate(&e));
 
-    // device copies of the record buffer (kept resident for steps 1 and 2)
+    // the record buffer, resident on device 0 for steps 1 and 2: parsed on the GPU
+    // from the raw file bytes, or parsed on the host and copied
+    kmc_fasta *fa = nullptr;
     char *d_data = nullptr;
     int64_t *d_idx = nullptr;
-    const size_t alloc = bytes > 0 ? bytes : 16;
-    HIPCHK(hipMalloc(&d_data, alloc));
-    HIPCHK(hipMalloc(&d_idx, (n + 1) * sizeof(int64_t)));
-    HIPCHK(hipEventRecord(ev[0], st));
-    if (bytes) HIPCHK(hipMemcpyAsync(d_data, kmc_fasta_data(fa), bytes, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(d_idx, hidx, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    HIPCHK(hipEventRecord(ev[1], st));
-
+    uint64_t n = 0, bytes = 0;
+    std::vector<int64_t> hidx;
+    const bool host = o.host_loader || o.gpus > 1;
+    const auto tl0 = std::chrono::steady_clock::now();
+    if (host) {
+        KMCCHK(kmc_fasta_load(o.input.c_str(), o.dialect, o.max_seqs, &fa));
+        n = kmc_fasta_num_seqs(fa);
+        bytes = kmc_fasta_data_bytes(fa);
+        hidx.assign(kmc_fasta_indices(fa), kmc_fasta_indices(fa) + n + 1);
+        HIPCHK(hipMalloc(&d_data, bytes + 16));
+        HIPCHK(hipMalloc(&d_idx, (n + 1) * sizeof(int64_t)));
+        if (bytes) HIPCHK(hipMemcpyAsync(d_data, kmc_fasta_data(fa), bytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(d_idx, hidx.data(), (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } else {
+        KMCCHK(kmc_fasta_load_device(o.input.c_str(), o.dialect, o.max_seqs, &d_data, &bytes, &d_idx, &n, st));
+        hidx.resize(n + 1);
+        HIPCHK(hipMemcpy(hidx.data(), d_idx, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    }
+    const auto tl1 = std::chrono::steady_clock::now();
+    if (!o.quiet) {
+        printf("K = %d\n", k);
+        printf("Size all seqs:%" PRIu64 "\n", bytes);  // main.cu:166-167
+        printf("%" PRIu64 " sequences read .\n", n);
+        printf("Load (%s parse, file to device): %.1f ms\n", host ? "host" : "GPU",
+               std::chrono::duration<double, std::milli>(tl1 - tl0).count());
+    }
     if (o.canonical) {
         const unsigned flags = o.softmask ? KMC_CANON_SOFTMASK : 0u;
         const uint64_t cap = bytes > 0 ? bytes : 1;
@@ -237,7 +251,6 @@ int run(const Options &o) {
         HIPCHK(hipEventRecord(ev[3], st));
         HIPCHK(hipStreamSynchronize(st));
         if (!o.quiet) {
-            printf("H2D: %.3f ms\n", ms_between(ev[0], ev[1]));
             printf("Canonical k=%d: %" PRIu64 " distinct (record, k-mer) pairs, %.3f ms\n", k, distinct,
                    ms_between(ev[2], ev[3]));
         }
@@ -261,7 +274,7 @@ int run(const Options &o) {
         HIPCHK(hipFree(d_off));
         HIPCHK(hipFree(d_data));
         HIPCHK(hipFree(d_idx));
-        kmc_fasta_free(fa);
+        if (fa) kmc_fasta_free(fa);
         return 0;
     }
 
@@ -271,7 +284,7 @@ int run(const Options &o) {
     int *d_idx32 = nullptr;
     if (o.dropin) {
         if (bytes > (uint64_t)INT32_MAX) return fprintf(stderr, "kmc: --dropin needs < 2 GiB of sequence\n"), 1;
-        std::vector<int> i32(hidx, hidx + n + 1);
+        std::vector<int> i32(hidx.begin(), hidx.end());
         HIPCHK(hipMalloc(&d_idx32, (n + 1) * sizeof(int)));
         HIPCHK(hipMemcpy(d_idx32, i32.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice));
     }
@@ -284,7 +297,7 @@ int run(const Options &o) {
     } else if (o.gpus > 1) {
         // host-buffer multi-GPU count (shards + RCCL all-reduce), result on the host
         hsum.assign(nb * n, 0);
-        KMCCHK(kmc_count_multi(kmc_fasta_data(fa), hidx, n, bytes, k, o.gpus, nullptr, hsum.data(), nullptr));
+        KMCCHK(kmc_count_multi(kmc_fasta_data(fa), hidx.data(), n, bytes, k, o.gpus, nullptr, hsum.data(), nullptr));
         if (!hsum.empty())
             HIPCHK(hipMemcpyAsync(d_sum, hsum.data(), hsum.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     } else {
@@ -294,7 +307,6 @@ int run(const Options &o) {
     HIPCHK(hipEventSynchronize(ev[3]));
     const float t1 = ms_between(ev[2], ev[3]);
     if (!o.quiet) {
-        printf("H2D: %.3f ms\n", ms_between(ev[0], ev[1]));
         printf("Elapsed parallel timer step 1: %g ms, %g secs\n", t1, t1 / 1000);  // main.cu:300
     }
 
@@ -343,7 +355,7 @@ int run(const Options &o) {
     HIPCHK(hipFree(d_idx));
     for (auto &e : ev) HIPCHK(hipEventDestroy(e));
     HIPCHK(hipStreamDestroy(st));
-    kmc_fasta_free(fa);
+    if (fa) kmc_fasta_free(fa);
     return 0;
 }
 

@@ -28,6 +28,7 @@ DIALECT_BLANK = 0  # importSeqs
 DIALECT_NONL = 1   # importSeqsNoNL
 MAX_SEQS_REFERENCE = 100
 DROPIN_K = 3
+KMC_ERR_CAPACITY = 1009
 
 
 class KmcError(RuntimeError):
@@ -86,6 +87,10 @@ def lib():
         L.kmc_fasta_data.argtypes = [_P]
         L.kmc_fasta_free.argtypes = [_P]
         L.kmc_fasta_free.restype = None
+        L.kmc_fasta_parse_device.argtypes = [_P, _U64, ctypes.c_int, _P, _U64, _P, _U64, ctypes.POINTER(_U64),
+                                             ctypes.POINTER(_U64), _P]
+        L.kmc_fasta_load_device.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P),
+                                            ctypes.POINTER(_U64), ctypes.POINTER(_P), ctypes.POINTER(_U64), _P]
         L.kmc_pair_distances_workspace_size.restype = ctypes.c_size_t
         L.kmc_pair_distances_workspace_size.argtypes = [_U64, ctypes.c_int, ctypes.c_int]
         L.kmc_pair_distances.argtypes = [_P, _U64, _P, _U64, ctypes.c_int, _P, _P, ctypes.c_size_t, _P]
@@ -313,6 +318,62 @@ def load_fasta(path, dialect=DIALECT_BLANK, max_seqs=MAX_SEQS_REFERENCE):
     finally:
         L.kmc_fasta_free(h)
     return data, idx, int(ref_n)
+
+
+def parse_fasta_device(raw, dialect=DIALECT_BLANK, stream=None):
+    """GPU FASTA parse (kmc_fasta_parse_device) of raw file bytes in a uint8 device
+    tensor; returns (data uint8 tensor, indices int64 tensor [n+1]) on its device."""
+    import torch
+    n = int(raw.numel())
+    if n % 16 or raw.data_ptr() % 16:  # the kernel reads whole 16-byte pieces of raw
+        pad = torch.zeros(n + 16 - n % 16, dtype=torch.uint8, device=raw.device)
+        pad[:n] = raw
+        raw = pad
+    data = torch.empty(n + 16, dtype=torch.uint8, device=raw.device)
+    cap = 1024
+    while True:
+        idx = torch.empty(cap, dtype=torch.int64, device=raw.device)
+        ns, nb = _U64(0), _U64(0)
+        rc = lib().kmc_fasta_parse_device(_dptr(raw) if n else None, n, dialect, _dptr(data), n + 16, _dptr(idx),
+                                          cap, ctypes.byref(ns), ctypes.byref(nb), _stream(stream))
+        if rc == KMC_ERR_CAPACITY and ns.value + 1 > cap:
+            cap = int(ns.value) + 1
+            continue
+        _check(rc, "kmc_fasta_parse_device")
+        return data[:nb.value], idx[:ns.value + 1]
+
+
+def load_fasta_device(path, dialect=DIALECT_BLANK, max_seqs=MAX_SEQS_REFERENCE, stream=None):
+    """kmc_fasta_load_device: (data uint8 tensor, indices int64 tensor [n+1]) on the
+    current device (copies of the library's buffers, which are freed here)."""
+    import torch
+    L = lib()
+    d, ix = _P(), _P()
+    nb, ns = _U64(0), _U64(0)
+    _check(L.kmc_fasta_load_device(os.fsencode(path), dialect, max_seqs, ctypes.byref(d), ctypes.byref(nb),
+                                   ctypes.byref(ix), ctypes.byref(ns), _stream(stream)), "kmc_fasta_load_device")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    data = torch.empty(nb.value, dtype=torch.uint8, device=dev)
+    idx = torch.empty(ns.value + 1, dtype=torch.int64, device=dev)
+    hip = _hip()
+    if nb.value:
+        _check(hip.hipMemcpy(_P(data.data_ptr()), d, nb.value, 3), "hipMemcpy")
+    _check(hip.hipMemcpy(_P(idx.data_ptr()), ix, (ns.value + 1) * 8, 3), "hipMemcpy")
+    hip.hipFree(d)
+    hip.hipFree(ix)
+    return data, idx
+
+
+_hip_lib = None
+
+
+def _hip():
+    global _hip_lib
+    if _hip_lib is None:
+        _hip_lib = ctypes.CDLL("libamdhip64.so")
+        _hip_lib.hipMemcpy.argtypes = [_P, _P, ctypes.c_size_t, ctypes.c_int]
+        _hip_lib.hipFree.argtypes = [_P]
+    return _hip_lib
 
 
 # ---------------------------------------------------------------------------

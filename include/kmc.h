@@ -244,6 +244,30 @@ uint64_t kmc_fasta_data_bytes(const kmc_fasta *f);
 uint64_t kmc_fasta_reference_num_indexes(const kmc_fasta *f);
 void kmc_fasta_free(kmc_fasta *f);
 
+/* FASTA parsing on the GPU: the record rules of
+ * kmc_fasta_load (importSeqs / importSeqsNoNL, main.cu:474-545 / 401-473) without
+ * the MAX_SEQS cap, applied to raw FASTA bytes already in device memory, at HBM
+ * speed instead of the reference's host getline loop.
+ *   raw       device, 16-byte aligned, raw_bytes bytes of FASTA text
+ *   data      device, 4-byte aligned, capacity data_cap >= raw_bytes + 1
+ *   indices   device int64[indices_cap]; num_seqs + 1 entries are written
+ * On return *num_seqs and *data_bytes describe the buffer exactly as
+ * kmc_fasta_load would; KMC_ERR_CAPACITY (with *num_seqs set) when indices_cap <
+ * *num_seqs + 1.  Synchronous on `stream`; library-owned scratch (~2 B per line). */
+int kmc_fasta_parse_device(const char *raw, uint64_t raw_bytes, int dialect, char *data, uint64_t data_cap,
+                           int64_t *indices, uint64_t indices_cap, uint64_t *num_seqs, uint64_t *data_bytes,
+                           hipStream_t stream);
+
+/* File -> device record buffer: reads `path` through pinned staging buffers
+ * into device memory (the read of one chunk overlapping the copy of the last) and
+ * parses it there (kmc_fasta_parse_device).  With max_seqs > 0 and more records
+ * than that, the reference's cap applies, which cuts mid-record; the file is then
+ * loaded by kmc_fasta_load and copied instead.  *data (*data_bytes + 16 bytes) and
+ * *indices (*num_seqs + 1 entries) are hipMalloc'ed; the caller hipFree's them.
+ * Synchronous on `stream`. */
+int kmc_fasta_load_device(const char *path, int dialect, int64_t max_seqs, char **data, uint64_t *data_bytes,
+                          int64_t **indices, uint64_t *num_seqs, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

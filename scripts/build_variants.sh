@@ -8,7 +8,7 @@ mkdir -p $PKG/lib/variants
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$ROOT/include -I$PKG/csrc $flags -shared \
-    -o $PKG/lib/variants/libkmc_$name.so $PKG/csrc/kmc_dense.hip $PKG/csrc/kmc_radix.hip $PKG/csrc/kmc_synth.hip $PKG/csrc/kmc_dist.hip $PKG/csrc/kmc_hash.hip \
+    -o $PKG/lib/variants/libkmc_$name.so $PKG/csrc/kmc_dense.hip $PKG/csrc/kmc_radix.hip $PKG/csrc/kmc_synth.hip $PKG/csrc/kmc_dist.hip $PKG/csrc/kmc_hash.hip $PKG/csrc/kmc_fasta_gpu.hip \
     -x none $PKG/build/kmc_common.o $PKG/build/kmc_fasta.o $PKG/build/kmc_multi.o -L/opt/rocm/lib -lrccl &
 done
 wait

@@ -35,3 +35,28 @@ def full_indices(g):
     if idx.size == n:
         idx = np.append(idx, np.int64(g["data"].size))
     return idx
+
+
+def random_fasta(rng, path, nrec_max=12):
+    """A small FASTA with the structures the reference's loader distinguishes:
+    blank lines between and inside records, headers, CRLF and '\r'-initial lines,
+    lowercase, N, '|', empty sequence lines, optionally no final newline."""
+    parts = []
+    for i in range(int(rng.integers(1, nrec_max))):
+        if rng.random() < 0.1:
+            parts.append("\n")
+        parts.append(">rec%d %s\n" % (i, "x" * int(rng.integers(0, 5))))
+        if rng.random() < 0.1:
+            parts.append("\n")
+        for _ in range(int(rng.integers(0, 5))):
+            L = int(rng.integers(0, 90))
+            s = "".join(rng.choice(list("ACGTNacgt|"), size=L, p=[.21, .21, .21, .21, .06, .02, .02, .02, .02, .02]))
+            eol = "\r\n" if rng.random() < 0.1 else "\n"
+            parts.append(s + eol)
+        if rng.random() < 0.7:
+            parts.append("\r\n" if rng.random() < 0.2 else "\n")
+    txt = "".join(parts)
+    if rng.random() < 0.3:
+        txt = txt.rstrip("\n")
+    with open(path, "w", newline="") as f:
+        f.write(txt)

@@ -31,35 +31,13 @@ def test_loader_quirks_documented(kmc):
     assert idx[-1] == d.size                            # we always carry it
 
 
-def _random_fasta(rng, path):
-    parts = []
-    for i in range(int(rng.integers(1, 12))):
-        if rng.random() < 0.1:
-            parts.append("\n")
-        parts.append(">rec%d %s\n" % (i, "x" * int(rng.integers(0, 5))))
-        if rng.random() < 0.1:
-            parts.append("\n")
-        for _ in range(int(rng.integers(0, 5))):
-            L = int(rng.integers(0, 90))
-            s = "".join(rng.choice(list("ACGTNacgt|"), size=L, p=[.21, .21, .21, .21, .06, .02, .02, .02, .02, .02]))
-            eol = "\r\n" if rng.random() < 0.1 else "\n"
-            parts.append(s + eol)
-        if rng.random() < 0.7:
-            parts.append("\r\n" if rng.random() < 0.2 else "\n")
-    txt = "".join(parts)
-    if rng.random() < 0.3:
-        txt = txt.rstrip("\n")
-    with open(path, "w", newline="") as f:
-        f.write(txt)
-
-
 @pytest.mark.parametrize("seed", range(40))
 def test_loader_matches_reference_live(kmc, oracle, tmp_path, seed):
     if not oracle.have_ref_cpu():
         pytest.skip("oracle/_ref not built (no /root/reference here)")
     rng = np.random.default_rng(seed)
     path = str(tmp_path / "r.fa")
-    _random_fasta(rng, path)
+    G.random_fasta(rng, path)
     for dialect in (0, 1):
         for cap in (kmc.MAX_SEQS_REFERENCE, 3):
             if cap != kmc.MAX_SEQS_REFERENCE:
