@@ -17,15 +17,18 @@
 // counting (--canonical).  GPU only: there is no CPU counting path here.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kmc.h"
+#include "kmc_internal.h"
 
 namespace {
 
@@ -48,6 +51,7 @@ struct Options {
 void usage(FILE *f) {
     fprintf(f,
             "usage: kmc [options] <input.fasta>\n"
+            "       kmc synth OUT.fa RECORDS LENGTH [SEED]   (benchmark input, SURVEY.md 8(d))\n"
             "  -k K              k-mer length (default %d, the reference's K); dense path 1..%d,\n"
             "                    --canonical 1..%d\n"
             "  --dialect D       blank (importSeqs: records end at blank lines, default) or\n"
@@ -359,9 +363,62 @@ int run(const Options &o) {
     return 0;
 }
 
+
+// `kmc synth OUT.fa RECORDS LENGTH [SEED]`: the SURVEY.md §8(d) benchmark input as a
+// FASTA file: records of LENGTH bases in 80 columns, '>r%04d' headers, records
+// separated by one blank line (the importSeqs dialect, also read by NoNL), no
+// final blank line.  Base g of the concatenated records is "ACGT"[(x_{g/32} >>
+// 2(g%32)) & 3], x_n = splitmix64 output n (kmc_synth_fill's stream, so the parsed
+// buffer equals kmc_synth_fill's).  Lines are generated by host threads.
+int synth_main(int argc, char **argv) {
+    if (argc < 5) return fprintf(stderr, "usage: kmc synth OUT.fa RECORDS LENGTH [SEED]\n"), 2;
+    const char *path = argv[2];
+    const uint64_t nrec = strtoull(argv[3], nullptr, 10), len = strtoull(argv[4], nullptr, 10);
+    const uint64_t seed = argc > 5 ? strtoull(argv[5], nullptr, 0) : 0x5EED0008ull;
+    FILE *f = fopen(path, "wb");
+    if (!f) return fprintf(stderr, "kmc: cannot write %s\n", path), 1;
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    constexpr uint64_t kBlockBases = 80ull << 20;  // whole lines per block
+    std::vector<std::string> buf(nth);
+    for (uint64_t r = 0; r < nrec; ++r) {
+        char hdr[32];
+        snprintf(hdr, sizeof hdr, "%s>r%04llu\n", r ? "\n" : "", (unsigned long long)r);
+        fputs(hdr, f);
+        for (uint64_t b0 = 0; b0 < len; b0 += kBlockBases * nth) {
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < nth; ++t) {
+                th.emplace_back([&, t]() {
+                    std::string &o = buf[t];
+                    o.clear();
+                    const uint64_t lo = b0 + t * kBlockBases;
+                    if (lo >= len) return;
+                    const uint64_t hi = std::min(len, lo + kBlockBases);
+                    o.reserve((hi - lo) + (hi - lo) / 80 + 2);
+                    for (uint64_t i = lo; i < hi; i += 80) {
+                        const uint64_t e = std::min(hi, i + 80);
+                        uint64_t xn = ~0ull, x = 0;
+                        for (uint64_t j = i; j < e; ++j) {
+                            const uint64_t g = r * len + j;
+                            if ((g >> 5) != xn) x = kmc::splitmix64_at(seed, xn = g >> 5);
+                            o.push_back("ACGT"[(x >> (2 * (g & 31))) & 3]);
+                        }
+                        o.push_back('\n');
+                    }
+                });
+            }
+            for (auto &x : th) x.join();
+            for (unsigned t = 0; t < nth; ++t)
+                if (!buf[t].empty() && fwrite(buf[t].data(), 1, buf[t].size(), f) != buf[t].size())
+                    return fclose(f), fprintf(stderr, "kmc: write failed\n"), 1;
+        }
+    }
+    return fclose(f) == 0 ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
+    if (argc > 1 && std::string(argv[1]) == "synth") return synth_main(argc, argv);
     Options o;
     const int rc = parse(argc, argv, o);
     if (rc) return rc;
