@@ -35,6 +35,12 @@
 #include "kmc_internal.h"
 #include "kmc_stream.h"
 
+// k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
+// spill entries (0: no scans)
+#ifndef KMC_HM3_SCAN
+#define KMC_HM3_SCAN 64
+#endif
+
 namespace kmc {
 thread_local hipEvent_t t_trace_before = nullptr;
 thread_local hipEvent_t t_trace_after = nullptr;
@@ -76,6 +82,7 @@ __device__ __forceinline__ uint32_t half_inc(uint32_t hb) {
 // Per-piece context of the k == 8 packed-16-bit histogram.
 struct P16Ctx {
     uint32_t *h;
+    uint32_t *spilled;  // LDS: increments moved to spill entries by scans (this piece)
     uint32_t *spill_n;  // LDS counter
     Spill *spill;       // this workgroup's slice
     uint32_t cap;
@@ -255,15 +262,20 @@ __device__ __noinline__ void p16_scan_fix(const P16Ctx &pc, int i4) {
         const uint32_t word = (uint32_t)(4 * i4 + q);
         const uint32_t x = w[q];
         const uint32_t lo = x & 0xFFFFu, hi = x >> 16;
-        if (lo >= T) p16_spill(pc, (int32_t)word, (int32_t)(lo & ~(T - 1)));
-        if (hi >= T) p16_spill(pc, (int32_t)(word | 0x8000u), (int32_t)(hi & ~(T - 1)));
+        if (lo >= T) {
+            p16_spill(pc, (int32_t)word, (int32_t)(lo & ~(T - 1)));
+            atomicAdd(pc.spilled, lo & ~(T - 1));
+        }
+        if (hi >= T) {
+            p16_spill(pc, (int32_t)(word | 0x8000u), (int32_t)(hi & ~(T - 1)));
+            atomicAdd(pc.spilled, hi & ~(T - 1));
+        }
         w[q] = (lo & (T - 1)) | ((hi & (T - 1)) << 16);
     }
 }
 
-template <int BLOCK>
+template <int BLOCK, uint32_t T>
 __device__ __forceinline__ void p16_scan(const P16Ctx &pc) {
-    constexpr uint32_t T = Scan<BLOCK>::kT;
     constexpr uint32_t HOT = (0xFFFFu & ~(T - 1)) * 0x00010001u;  // bits >= T in both halves
     constexpr int NW4 = (1 << 15) / 4;  // 32768 words as uint4
     const uint4 *h4 = reinterpret_cast<const uint4 *>(pc.h);
@@ -306,10 +318,21 @@ struct DenseOp {
         if constexpr (HM == 1) {
             if (pending && i + 1 == per) p16_check(pc, pd);
         }
+        if constexpr (HM == 3 && KMC_HM3_SCAN > 0) {
+            // hot halves (>= 32768) go to spill entries every KMC_HM3_SCAN tiles per
+            // wave, so a half wraps only if one k-mer takes >= 32768 of the
+            // workgroup's NWAVES * KMC_HM3_SCAN * 1024 windows in between (long
+            // low-complexity runs); wraps stay detected by the piece total
+            if ((i % KMC_HM3_SCAN) == KMC_HM3_SCAN - 1 && i + 1 < per) {
+                lds_barrier();
+                p16_scan<BLOCK, 32768u>(pc);
+                lds_barrier();
+            }
+        }
         if constexpr (HM == 2) {
             if ((i % Scan<BLOCK>::kTiles) == Scan<BLOCK>::kTiles - 1 && i + 1 < per) {
                 lds_barrier();
-                p16_scan<BLOCK>(pc);
+                p16_scan<BLOCK, Scan<BLOCK>::kT>(pc);
                 lds_barrier();
             }
         }
@@ -356,9 +379,11 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                     else hi = mid - 1;
                 }
             }
-            misc[0] = 0u;
+            // fallback launch: append to the first pass's spill entries
+            misc[0] = p.fallback ? p.spill_cnt[w] : 0u;
             misc[3] = 0u;
             misc[4] = 0u;
+            misc[5] = 0u;
             misc[1] = (uint32_t)lo;
             misc[2] = (uint32_t)((uint64_t)lo >> 32);
         }
@@ -366,8 +391,10 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
         __syncthreads();
         const int64_t s0 = (int64_t)((uint64_t)misc[1] | ((uint64_t)misc[2] << 32));
 
+        const uint32_t first_spills = misc[0];
         P16Ctx pc;
         pc.h = h;
+        pc.spilled = misc + 5;
         pc.spill_n = misc;
         pc.spill = p.spill ? p.spill + (int64_t)w * p.spill_cap : nullptr;
         pc.cap = p.spill_cap;
@@ -388,6 +415,13 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 }
             }
             pc.rec = s;
+            if (p.fallback && pc.spill) {
+                // the first pass's scan entries of this piece are superseded by the recount
+                const uint32_t nold = first_spills < pc.cap ? first_spills : pc.cap;
+                for (uint32_t i = tid; i < nold; i += BLOCK)
+                    if (pc.spill[i].rec == s) pc.spill[i].amount = 0;
+                __syncthreads();
+            }
             // this piece's tiles, split into contiguous per-wave runs
             const int64_t tp0 = ps >> kTileShift;
             const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
@@ -442,11 +476,13 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             __syncthreads();
             if constexpr (HM == 3) {
                 // every 16-bit wrap only loses counts (low half: -65535 net, high half:
-                // -65536), so the decoded total equals the windows added iff none wrapped
+                // -65536), so the decoded total plus the scans' spills equals the
+                // windows added iff none wrapped
                 if (tid == 0) {
-                    if (misc[3] != misc[4]) failed |= npieces < 63 ? (1ull << npieces) : (1ull << 63);
+                    if (misc[3] != misc[4] + misc[5]) failed |= npieces < 63 ? (1ull << npieces) : (1ull << 63);
                     misc[3] = 0u;
                     misc[4] = 0u;
+                    misc[5] = 0u;
                 }
                 __syncthreads();
             }

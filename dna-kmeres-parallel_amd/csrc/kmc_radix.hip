@@ -34,6 +34,11 @@
 #ifndef KMC_RSCAT_ABL
 #define KMC_RSCAT_ABL 0
 #endif
+// tile prefetch depth of the scatter pass (register pressure: the round's windows
+// stay in registers across the barrier)
+#ifndef KMC_RSCAT_PF
+#define KMC_RSCAT_PF 2
+#endif
 
 namespace kmc {
 namespace {
@@ -80,11 +85,11 @@ struct RCountOp {
 
 // R3 op.  Scattering every window straight to its list costs one L2 write
 // request per 2-byte entry (64 per wave store); instead each round of one tile
-// per wave is staged in LDS, counting-sorted by bucket, and written out so that
-// consecutive lanes store consecutive entries of one list.
-//   buf  [NW][1024]  the round's codes, wave w in its own 1024-entry region
-//   srt  [NW*1024]   the round sorted by bucket (aliases buf: buf is read into
-//                    registers before srt is written)
+// per wave is counting-sorted by bucket in LDS and written out so that
+// consecutive lanes store consecutive entries of one list.  A window's rank in
+// its bucket is taken (returning LDS add) as the tile is decoded, and the window
+// stays in registers (code + rank) until the round's scan has placed the buckets.
+//   srt  [NW*1024]   the round sorted by bucket
 //   off  [NBK + 1]   bucket counts -> exclusive offsets within srt
 //   gcur [NBK]       global position of each list's next entry (this workgroup)
 //   gdel [NBK]       this round: global position of srt index 0 of each bucket's run
@@ -94,64 +99,47 @@ struct RStageOp {
     static constexpr int LOW = low_bits(K);
     static constexpr int NBK = 1 << (2 * K - LOW);
     static constexpr int BATCH = NW * 1024;
-    uint32_t *buf, *srt, *off, *nw;
+    static constexpr uint32_t kNone = 0xFFFFFFFFu;
+    uint32_t *srt, *off, *nw;
     unsigned long long *gcur;
     long long *gdel;
     uint16_t *ent;
     uint32_t b_lo, b_n;
     int wave, lane, tid;
-    uint32_t fill;  // entries of this wave in the current round (wave-uniform)
+    uint32_t code[16];  // this round's windows of the lane (kNone: none)
+    uint32_t rank[8];   // their ranks in their buckets, two 16-bit ranks per word (< BATCH)
 
     __device__ void before_tile() {}
 
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
-        uint32_t *dst = buf + wave * 1024;
-        uint32_t run = 0;
-        const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const uint32_t code = window_code_rt<K>(lo, hi, j);
-            const bool v = (!MASKED || ((W >> j) & 1u)) && ((code >> LOW) - b_lo) < b_n;
-            const uint64_t m = __ballot(v);
-            if (v) dst[run + __popcll(m & lt)] = code;
-            run += __popcll(m);
+            const uint32_t c = window_code_rt<K>(lo, hi, j);
+            const bool v = (!MASKED || ((W >> j) & 1u)) && ((c >> LOW) - b_lo) < b_n;
+            uint32_t r = 0;
+            if (v) r = __hip_atomic_fetch_add(&off[(c >> LOW) - b_lo], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            code[j] = v ? c : kNone;
+            if (j & 1) rank[j >> 1] |= r << 16;
+            else rank[j >> 1] = r;
         }
-        fill = run;
     }
 
-    __device__ void after_iter(int64_t, int64_t, bool active) {
-        if (lane == 0) nw[wave] = active ? fill : 0u;
-        fill = 0;
-        lds_barrier();
+    __device__ void after_iter(int64_t, int64_t, bool) {
+        lds_barrier();  // every rank taken
 #if KMC_RSCAT_ABL == 3
-        return;  // diagnostic: staging only
-#endif
-        // 1. rank of every staged entry within its bucket
-        const uint32_t mine = nw[wave];
-        uint32_t code[16], rank[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t e = (uint32_t)(j * 64 + lane);
-            code[j] = e < mine ? buf[wave * 1024 + e] : 0xFFFFFFFFu;
-#if KMC_RSCAT_ABL == 2
-            rank[j] = 0;
-            if (e < mine) __hip_atomic_fetch_add(&off[(code[j] >> LOW) - b_lo], 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-            if (e < mine)
-                rank[j] = __hip_atomic_fetch_add(&off[(code[j] >> LOW) - b_lo], 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-        }
+        for (int j = 0; j < 16; ++j) code[j] = kNone;
         lds_barrier();
-        // 2. exclusive scan of the bucket counts (off[b_n] = round total)
+        return;  // diagnostic: ranking only
+#endif
+        // exclusive scan of the bucket counts (off[b_n] = round total)
         block_scan_inplace(off, (int)b_n);
-        // 3. counting-sort the round into srt; per bucket, the global position of
-        //    srt index 0 (gdel = cursor - offset) and the advanced cursor
+        // counting-sort the round into srt; per bucket, the global position of srt
+        // index 0 (gdel = cursor - offset) and the advanced cursor
 #pragma unroll
         for (int j = 0; j < 16; ++j)
-            if (code[j] != 0xFFFFFFFFu) srt[off[(code[j] >> LOW) - b_lo] + rank[j]] = code[j];
+            if (code[j] != kNone)
+                srt[off[(code[j] >> LOW) - b_lo] + ((rank[j >> 1] >> (16 * (j & 1))) & 0xFFFFu)] = code[j];
         for (uint32_t b = tid; b < b_n; b += NW * 64) {
             const uint32_t o0 = off[b], o1 = off[b + 1];
             const unsigned long long g = gcur[b];
@@ -160,26 +148,23 @@ struct RStageOp {
         }
         const uint32_t total = off[b_n];
         lds_barrier();
-        // 4. coalesced write-out: srt[i] is entry i + gdel[b] of bucket b's list; the
-        //    counts are cleared for the next round (nothing reads them until then)
+        // coalesced write-out: srt[i] is entry i + gdel[b] of bucket b's list; the
+        // counts are cleared for the next round (nothing reads them until then)
         for (uint32_t b = tid; b <= b_n; b += NW * 64) off[b] = 0u;
-        uint32_t c[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const uint32_t i = tid + q * NW * 64;
-            c[q] = i < total ? srt[i] : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            if (c[q] == 0xFFFFFFFFu) continue;
-            const uint32_t i = tid + q * NW * 64;
-            const long long pos = gdel[(c[q] >> LOW) - b_lo] + (long long)i;
+            const uint32_t c = i < total ? srt[i] : kNone;
+            if (c == kNone) continue;
+            const long long pos = gdel[(c >> LOW) - b_lo] + (long long)i;
 #if KMC_RSCAT_ABL >= 1
-            if (c[q] == 0xFFFFFFFEu)  // diagnostic: never true, keeps the loads
+            if (c == 0xFFFFFFFEu)  // diagnostic: never true, keeps the loads
 #endif
-            ent[pos] = (uint16_t)(c[q] & ((1u << LOW) - 1));
+            ent[pos] = (uint16_t)(c & ((1u << LOW) - 1));
         }
-        lds_barrier();  // srt aliases buf: the next round's staging starts after every read
+#pragma unroll
+        for (int j = 0; j < 16; ++j) code[j] = kNone;
+        lds_barrier();  // srt and the counts are free for the next round
     }
 
     // in-place exclusive scan of a[0..m) with a[m] = total; all NW*64 threads
@@ -225,7 +210,7 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
     __shared__ int64_t s_first;
     uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds64);
     constexpr int SB = SCATTER ? NWAVES * 1024 : 1;
-    __shared__ __attribute__((aligned(16))) uint32_t s_buf[SB];
+    __shared__ __attribute__((aligned(16))) uint32_t s_srt[SB];
     __shared__ uint32_t s_off[SCATTER ? NBK + 1 : 1];
     __shared__ long long s_gdel[SCATTER ? NBK : 1];
     __shared__ uint32_t s_nw[2 * NWAVES];
@@ -265,9 +250,11 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         if constexpr (SCATTER) {
-            RStageOp<K, NWAVES> op{s_buf, s_buf, s_off, s_nw, lds64, s_gdel, p.ent, (uint32_t)p.b_lo,
-                                   (uint32_t)(p.b_hi - p.b_lo), wave, lane, tid, 0u};
-            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+            RStageOp<K, NWAVES> op{s_srt, s_off, s_nw, lds64, s_gdel, p.ent, (uint32_t)p.b_lo,
+                                   (uint32_t)(p.b_hi - p.b_lo), wave, lane, tid, {}, {}};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) op.code[j] = RStageOp<K, NWAVES>::kNone;
+            stream_tiles<K, RStageOp<K, NWAVES>, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         } else {
             RCountOp<K> op{lds32};
             stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);

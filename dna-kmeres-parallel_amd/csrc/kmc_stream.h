@@ -271,9 +271,9 @@ __device__ __forceinline__ uint4 mask_range(uint4 v, int64_t q, int64_t rl, int6
 // r[q+1]) or a load inside a branch make the compiler wait for the load it has
 // just issued (s_waitcnt vmcnt(0)) before the next decode, which leaves one tile
 // in flight per wave whatever KMC_PF says.
-template <int K>
+template <int K, int PF_ = KMC_PF>
 struct TileStream {
-    static constexpr int PF = KMC_PF;
+    static constexpr int PF = PF_;
     static constexpr int NS = PF + 1;
     const char *__restrict__ data;
     int64_t t0, ps, pe, rl, rh;
@@ -355,10 +355,10 @@ struct TileStream {
     }
 };
 
-template <int K, class Op>
+template <int K, class Op, int PF = KMC_PF>
 __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
                                              int64_t ps, int64_t pe, int64_t rl, int64_t rh, int lane, Op &op) {
-    using TS = TileStream<K>;
+    using TS = TileStream<K, PF>;
     const int64_t n = t1 > t0 ? t1 - t0 : 0;  // <= per
     if (n > 0) {
         TS ts;

@@ -12,6 +12,10 @@
 //   mode 7  ds_add_rtn_u32, random word (returning form)
 //   mode 8  ds_add_u32, random word of a 64 KiB table (16 384 words: k = 7, R = 1)
 //   mode 9  ds_add_u32, two lanes of each 32-lane group on a shared bank (2-way conflict, fixed)
+//   mode 10 ds_add_u32, random word of 16 384, 2 replicas interleaved by lane parity (32 768 words)
+//   mode 11 ds_add_u32, random word of 8 192, 4 replicas interleaved by lane % 4
+//   mode 12 ds_add_u32, random word of 32 768, replica-free, but only lanes 0-31 active
+//   mode 13 ds_add_u64, random qword of 8 192, 2 replicas interleaved by lane parity
 // Build: hipcc --offload-arch=gfx950 -O3 -o lds_microbench scripts/lds_microbench.hip
 // Run:   ./lds_microbench      (one JSON line per mode)
 #include <hip/hip_runtime.h>
@@ -79,6 +83,18 @@ __global__ __launch_bounds__(BLOCK) void lds_kernel(int iters, uint32_t *out) {
                 acc += __hip_atomic_fetch_add(&h[r & 0x7FFFu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else if constexpr (MODE == 8) {
                 __hip_atomic_fetch_add(&h[r & 0x3FFFu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if constexpr (MODE == 10) {
+                __hip_atomic_fetch_add(&h[((r & 0x3FFFu) << 1) | (lane & 1)], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if constexpr (MODE == 11) {
+                __hip_atomic_fetch_add(&h[((r & 0x1FFFu) << 2) | (lane & 3)], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if constexpr (MODE == 12) {
+                if (lane < 32)
+                    __hip_atomic_fetch_add(&h[r & 0x7FFFu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if constexpr (MODE == 13) {
+                __hip_atomic_fetch_add(&h64[((r & 0x1FFFu) << 1) | (lane & 1)], 0x0000000100000001ull,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else if constexpr (MODE == 9) {
                 __hip_atomic_fetch_add(&h[((r & 0x3FFu) << 5) | ((lane & 31) >> 1)], 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -137,6 +153,10 @@ int main() {
     r |= run<7>(cus, iters, out, "add_rtn_u32 random");
     r |= run<8>(cus, iters, out, "add_u32 random 16K words");
     r |= run<9>(cus, iters, out, "add_u32 2-way conflict");
+    r |= run<10>(cus, iters, out, "add_u32 random, 2 replicas by lane parity");
+    r |= run<11>(cus, iters, out, "add_u32 random, 4 replicas by lane%4");
+    r |= run<12>(cus, iters, out, "add_u32 random, lanes 0-31 only");
+    r |= run<13>(cus, iters, out, "add_u64 random, 2 replicas by lane parity");
     CHECK(hipFree(out));
     return r;
 }

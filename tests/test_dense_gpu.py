@@ -199,6 +199,36 @@ def test_k8_overflow_fallback_mixed(kmc, oracle, cuda):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
+def test_k8_hot_half_scans_with_fallback(kmc, oracle, cuda):
+    """k = 8, 400 MB: "hot" records (65 % A: AAAAAAAA is 3 % of the windows, > 65 536
+    per workgroup piece) are kept exact by the periodic hot-half scans (spill
+    entries, no wrap), while "burst" records (a multi-MB poly-A run, > 32 768 adds
+    between two scans) wrap and are recounted; workgroups holding both kinds of
+    piece keep the scans' spills of the first and drop those of the second."""
+    rng = np.random.default_rng(808)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+
+    def hot(n):
+        return np.where(rng.random(n) < 0.65, ord("A"), acgt[rng.integers(1, 4, n)]).astype(np.uint8)
+
+    def burst(n, run):
+        x = hot(n)
+        o = (n - run) // 2
+        x[o:o + run] = ord("A")
+        return x
+
+    seqs = [hot(100 << 20), burst(5 << 20, 3 << 20), hot(60 << 20), acgt[rng.integers(0, 4, 20 << 20)],
+            burst(3 << 20, 1 << 20), hot(150 << 20), burst(7 << 20, 5 << 20), hot(40 << 20)]
+    recs = [np.append(x, np.uint8(0)) for x in seqs]
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    got, inv = run_dense(kmc, cuda, data, idx, 8)
+    exp, exp_inv = oracle.count_dense(data, idx, 8)
+    assert exp[0].max() > 1 << 22
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
 @pytest.mark.parametrize("k", [4, 8])
 def test_range_shards_sum_to_full(kmc, oracle, cuda, k):
     """kmc_count_dense_ex over disjoint window ranges, each reading only its
