@@ -209,6 +209,9 @@ def main():
             chunk = data[off: off + S].cpu().numpy()
             host.append(np.append(chunk, np.uint8(0)))  # one record of S bases + terminator
         rate, kind, dt, kmers = cpu_baseline(host, k, threads)
+        # the same code on one thread (a quarter of one sample)
+        one = [np.append(host[0][: max(S // 4, k + 1)], np.uint8(0))]
+        rate1, _, dt1, _ = cpu_baseline(one, k, 1)
         import platform
         cpu_model = platform.processor()
         try:
@@ -221,9 +224,11 @@ def main():
             pass
         result["cpu_baseline"] = {
             "value": rate, "unit": "k-mers/s", "cores": threads, "kind": kind,
+            "value_1thread": rate1,
             "sample": "%d threads x %d bases of the same synthetic records (%.0f s wall, %d k-mers), "
-                      "k=%d, permutationsCountAll (substr + std::map, main.cu:636-646) -O2; CPU: %s"
-                      % (threads, S, dt, kmers, k, cpu_model),
+                      "k=%d, permutationsCountAll (substr + std::map, main.cu:636-646) -O2; value_1thread: "
+                      "1 thread x %d bases (%.1f s); CPU: %s"
+                      % (threads, S, dt, kmers, k, one[0].size - 1, dt1, cpu_model),
         }
     if rank == 0:
         print(json.dumps(result))

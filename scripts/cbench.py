@@ -47,6 +47,77 @@ def grch38_like(torch, dev, gbases, seed=38):
     return data, offs.to(dev), lens
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "?"
+
+
+def threads_used():
+    return min(16, len(os.sched_getaffinity(0)))
+
+
+def c3_cpu_baseline(data, L, k, sample):
+    """The reference's own CPU path (permutationsCountAll via oracle/_ref) at k = 13
+    on `threads` disjoint samples of the same records; the std::map of 4^k patterns
+    is built once beforehand and timed separately."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    sys.path.insert(0, repo)
+    import numpy as np
+    import oracle
+    import bench
+    if not oracle.have_ref_cpu():
+        return None
+    t0 = time.perf_counter()
+    oracle.ref_cpu().ref_build_map(k)
+    build_s = time.perf_counter() - t0
+    th = threads_used()
+    host = [np.append(data[(t % 10) * (L + 1) + (t // 10) * sample:][:sample].cpu().numpy(), np.uint8(0))
+            for t in range(th)]
+    rate, kind, dt, kmers = bench.cpu_baseline(host, k, th)
+    return {"value": rate, "unit": "k-mers/s", "cores": th, "kind": kind, "map_build_s": build_s,
+            "sample": "%d threads x %d bases of the same records (%.1f s wall, %d k-mers), permutationsCountAll "
+                      "(main.cu:636-646); the 4^%d-entry std::map built once in %.1f s (not in the rate); CPU: %s"
+                      % (th, sample, dt, kmers, k, build_s, cpu_model())}
+
+
+def c4_cpu_baseline(data, idx, k, sample):
+    """No reference counterpart (the reference stops at dense tables): the oracle's
+    C restatement (per record: keys, sort, run-length) on `threads` samples."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import threading
+    import numpy as np
+    import oracle
+    th = threads_used()
+    bufs = []
+    for t in range(th):
+        o = int(idx[t % (idx.numel() - 1)].item()) + (t // (idx.numel() - 1)) * sample
+        bufs.append(np.append(data[o:o + sample].cpu().numpy(), np.uint8(0)))
+    res = [None] * th
+
+    def work(i):
+        b = bufs[i]
+        res[i] = oracle.count_canonical(b, np.array([0, b.size], dtype=np.int64), k, soft=True)
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(th)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    kmers = sum(max(0, b.size - k) for b in bufs)
+    return {"value": kmers / dt, "unit": "k-mers/s", "cores": th, "kind": "port",
+            "sample": "%d threads x %d bases of the same records (%.1f s wall), oracle_count_canonical "
+                      "(oracle/kmc_oracle.c: keys, qsort, run-length; no reference counterpart); CPU: %s"
+                      % (th, sample, dt, cpu_model())}
+
+
 def timed(torch, fn, iters):
     fn()
     torch.cuda.synchronize()
@@ -68,6 +139,8 @@ def main():
     ap.add_argument("--gbases-c3", type=float, default=10.0)
     ap.add_argument("--gbases-c4", type=float, default=3.1)
     ap.add_argument("--k3", type=int, default=13)
+    ap.add_argument("--cpu-sample-c3", type=int, default=2_000_000, help="bases per CPU thread (0 = skip)")
+    ap.add_argument("--cpu-sample-c4", type=int, default=16_000_000, help="bases per CPU thread (0 = skip)")
     a = ap.parse_args()
     import torch
     import kmc
@@ -87,9 +160,11 @@ def main():
         med, best = timed(torch, lambda: kmc.count_dense_ex(args), a.iters)
         kmers = recs * (L - k + 1)
         alg = data.numel() + 4 * (1 << (2 * k)) * recs
-        print(json.dumps({"config": "C3", "k": k, "records": recs, "bases": recs * L, "s_med": med, "s_min": best,
-                          "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9,
-                          "frac8TB": alg / med / 8e12}), flush=True)
+        line = {"config": "C3", "k": k, "records": recs, "bases": recs * L, "s_med": med, "s_min": best,
+                "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9, "frac8TB": alg / med / 8e12}
+        if a.cpu_sample_c3 > 0:
+            line["cpu_baseline"] = c3_cpu_baseline(data, L, k, a.cpu_sample_c3)
+        print(json.dumps(line), flush=True)
         del data, out, ws, args
         torch.cuda.empty_cache()
     if "c4" in cfgs:
@@ -104,10 +179,12 @@ def main():
         keys, counts, off = res["r"]
         tot = int(counts.sum().item())
         alg = 17 * kmers  # 1 B input + 16 B table slot per k-mer
-        print(json.dumps({"config": "C4", "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
-                          "valid_windows": tot, "distinct": int(keys.numel()), "s_med": med, "s_min": best,
-                          "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9,
-                          "frac8TB": alg / med / 8e12}), flush=True)
+        line = {"config": "C4", "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
+                "valid_windows": tot, "distinct": int(keys.numel()), "s_med": med, "s_min": best,
+                "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9, "frac8TB": alg / med / 8e12}
+        if a.cpu_sample_c4 > 0:
+            line["cpu_baseline"] = c4_cpu_baseline(data, idx, k, a.cpu_sample_c4)
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
