@@ -210,16 +210,21 @@ __global__ __launch_bounds__(kWalkBlock) void canon_scatter_kernel(HParams p) {
     });
 }
 
-// list boundaries: list (r, b) = off[cbase_r + b*nwg_r] .. off[cbase_r + (b+1)*nwg_r]
+// list boundaries: list (r, b) = off[cbase_r + b*nwg_r] .. off[cbase_r + (b+1)*nwg_r];
+// one thread per list (lbase is sorted: the record is a binary search)
 __global__ void canon_list_start_kernel(HParams p) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r > p.n) return;
-    if (r == p.n) {
-        p.list_start[p.lists] = p.off[p.cbase[p.n]];  // = off[M], every entry
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l > p.lists) return;
+    if (l == p.lists) {
+        p.list_start[l] = p.off[p.cbase[p.n]];  // = off[M], every entry
         return;
     }
-    const int nb = 1 << p.lg[r];
-    for (int b = 0; b < nb; ++b) p.list_start[p.lbase[r] + b] = p.off[p.cbase[r] + (int64_t)b * p.nwg[r]];
+    int64_t a = 0, b = p.n - 1;  // last record r with lbase[r] <= l
+    while (a < b) {
+        const int64_t m = (a + b + 1) >> 1;
+        if (p.lbase[m] <= l) a = m; else b = m - 1;
+    }
+    p.list_start[l] = p.off[p.cbase[a] + (l - p.lbase[a]) * p.nwg[a]];
 }
 
 // K4: one workgroup per list.  Pass q of P counts the keys whose hash bits
@@ -243,23 +248,36 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
         if (tid == 0) s_misc[0] = 0u;  // overflow flag
         __syncthreads();
         const uint32_t lgP = 31 - __builtin_clz(P);
-        for (uint64_t i = beg + tid; i < end; i += kCountBlock) {
-            const uint64_t key = p.ent[i];
-            const uint64_t h = fmix64(key);
-            if (lgP && (uint32_t)((h >> 32) & (P - 1)) != q) continue;
-            uint32_t s = (uint32_t)(((h & 0xFFFFFFFFull) * kTableSlots) >> 32);
-            uint32_t probes = 0;
-            for (;;) {
-                const unsigned long long cur = atomicCAS(&tk[s], kEmpty, (unsigned long long)key);
-                if (cur == kEmpty || cur == key) {
-                    __hip_atomic_fetch_add(&tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    break;
+        // the list in batches of kBatch keys per thread: all loads of a batch are in
+        // flight together (one HBM latency per batch, not per key)
+        constexpr int kBatch = 8;
+        for (uint64_t i0 = beg; i0 < end; i0 += (uint64_t)kBatch * kCountBlock) {
+            unsigned long long kb[kBatch];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) {
+                const uint64_t i = i0 + (uint64_t)j * kCountBlock + tid;
+                kb[j] = i < end ? p.ent[i] : kEmpty;
+            }
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j) {
+                const unsigned long long key = kb[j];
+                if (key == kEmpty) continue;
+                const uint64_t h = fmix64(key);
+                if (lgP && (uint32_t)((h >> 32) & (P - 1)) != q) continue;
+                uint32_t s = (uint32_t)(((h & 0xFFFFFFFFull) * kTableSlots) >> 32);
+                uint32_t probes = 0;
+                for (;;) {
+                    const unsigned long long cur = atomicCAS(&tk[s], kEmpty, key);
+                    if (cur == kEmpty || cur == key) {
+                        __hip_atomic_fetch_add(&tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        break;
+                    }
+                    if (++probes == kTableSlots) {  // table full: this pass splits in two
+                        s_misc[0] = 1u;
+                        break;
+                    }
+                    s = s + 1 == (uint32_t)kTableSlots ? 0u : s + 1;
                 }
-                if (++probes == kTableSlots) {  // table full: this pass splits in two
-                    s_misc[0] = 1u;
-                    break;
-                }
-                s = s + 1 == (uint32_t)kTableSlots ? 0u : s + 1;
             }
         }
         __syncthreads();
@@ -458,7 +476,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     }
     excl_scan_u32(p.cnt, M, bsum, p.off, stream);
     hipLaunchKernelGGL(canon_scatter_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
-    hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
     hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)L), dim3(kCountBlock), 0, stream, p);
     excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);
     hipLaunchKernelGGL(canon_recoff_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
