@@ -40,8 +40,13 @@ namespace kmc {
 namespace {
 
 constexpr uint64_t kEmpty = ~0ull;           // no k-mer key reaches it (62 bits at most)
+// K3 walks a piece once per group of lists, 2^KMC_CANON_SCATTER_LG groups at
+// most (write locality, see K3)
+#ifndef KMC_CANON_SCATTER_LG
+#define KMC_CANON_SCATTER_LG 2
+#endif
 constexpr int kWalkBlock = 1024;             // K1 / K3 threads per workgroup
-constexpr int kMaxLg = 14;                   // at most 16 384 lists per record (64-bit cursors: 128 KB LDS)
+constexpr int kMaxLg = 14;                   // at most 16 384 lists per record (more lists: more open write segments in K3)
 constexpr int64_t kListTarget = 4096;        // windows per list aimed at
 constexpr int kCountBlock = 1024;            // K4 threads per workgroup
 constexpr int kTableSlots = 12288;           // K4 LDS table: 12 288 x (8 + 4) B = 144 KB
@@ -192,20 +197,33 @@ __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
 
 // K3: every window's key at its list position
 __global__ __launch_bounds__(kWalkBlock) void canon_scatter_kernel(HParams p) {
-    __shared__ unsigned long long cur[1 << kMaxLg];
+    __shared__ uint32_t cur[1 << kMaxLg];  // relative to the record's first entry (< 2^32 per record)
     __shared__ int64_t s_first;
     const int w = blockIdx.x;
     for_each_piece(p, &s_first, [&](int64_t r, int64_t ps, int64_t pe, int64_t rend) {
         const int lg = p.lg[r];
         const int nb = 1 << lg;
         const int64_t base = p.cbase[r] + (w - p.w0[r]);
-        for (int b = threadIdx.x; b < nb; b += kWalkBlock) cur[b] = p.off[base + (int64_t)b * p.nwg[r]];
+        const uint64_t rbase = p.off[p.cbase[r]];
+        for (int b = threadIdx.x; b < nb; b += kWalkBlock)
+            cur[b] = (uint32_t)(p.off[base + (int64_t)b * p.nwg[r]] - rbase);
         __syncthreads();
-        walk_piece(p, ps, pe, rend, [&](uint64_t key) {
-            const unsigned long long i = __hip_atomic_fetch_add(&cur[list_of(key, lg)], 1ull, __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_WORKGROUP);
-            p.ent[i] = key;
-        });
+        uint64_t *ent = p.ent + rbase;
+        // the piece is walked once per group of lists: a workgroup keeps one
+        // partially written 128-B line open per list it writes, and with all of a
+        // record's lists open on every workgroup those lines overflow the
+        // Infinity Cache, turning each 8-B key store into a read-modify-write in HBM
+        const int glg = lg < KMC_CANON_SCATTER_LG ? lg : KMC_CANON_SCATTER_LG;  // log2 groups
+        const int gshift = lg - glg;
+        const uint32_t ng = 1u << glg;
+        for (uint32_t g = 0; g < ng; ++g) {
+            walk_piece(p, ps, pe, rend, [&](uint64_t key) {
+                const uint32_t l = list_of(key, lg);
+                if ((l >> gshift) != g) return;
+                const uint32_t i = __hip_atomic_fetch_add(&cur[l], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ent[i] = key;
+            });
+        }
         __syncthreads();
     });
 }
@@ -268,7 +286,8 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
                 uint32_t probes = 0;
                 for (;;) {
                     const unsigned long long cur = atomicCAS(&tk[s], kEmpty, key);
-                    if (cur == kEmpty || cur == key) {
+                    if (cur == kEmpty) break;  // claimed: first occurrence (tc holds occurrences - 1)
+                    if (cur == key) {
                         __hip_atomic_fetch_add(&tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         break;
                     }
@@ -313,7 +332,7 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
             const unsigned long long key = tk[tid * PER + j];
             if (key != kEmpty) {
                 p.pk[o2] = key;
-                p.pc[o2] = tc[tid * PER + j];
+                p.pc[o2] = tc[tid * PER + j] + 1u;
                 ++o2;
             }
         }
