@@ -7,24 +7,31 @@
 // min(key(window), key(reverse complement)) unless KMC_CANON_FORWARD is given.
 //
 // Hash-partitioned counting, so that no table lives in HBM and no k-mer costs a
-// device-scope atomic:
+// device-scope atomic.  A window travels as h = fmix64(key) (a bijection; only the
+// distinct keys are unmixed, at output).  Record r has 2^lg_r lists (top lg_r bits
+// of h, about 4 K windows each, lg_r <= 14), grouped in 2^lgc_r coarse buckets
+// (top lgc_r = min(lg_r, 7) bits):
 //   K1 count    workgroups walk contiguous chunk ranges record piece by record
-//               piece; each window's list is (record r, top bits of fmix64(key)),
-//               nb_r = 2^lg_r lists per record (about 4 K windows each); per-piece
-//               LDS counters -> cnt[(r, list, workgroup)]
-//   K2 scan     exclusive prefix sum: every list contiguous, workgroup segments
-//               inside it (kmc_scan.h)
-//   K3 scatter  the same walk writes each window's key at its list position
-//               (LDS 64-bit cursors per list)
-//   K4 count    one workgroup per list: an LDS open-addressing table (64-bit CAS
-//               claim, 32-bit add) counts the list, in as many passes over it as
-//               keep a pass's distinct keys under the table's capacity (selected
-//               by further hash bits); each pass's (key, count) pairs are compacted
-//               to the list's output segment; distinct keys per list
+//               piece; per-piece LDS counters -> windows per (r, list, workgroup)
+//               and per (r, coarse bucket, workgroup)
+//   K2 scan     exclusive prefix sums of both (kmc_scan.h): lists contiguous,
+//               coarse buckets = runs of lists, workgroup segments inside each
+//   K3a coarse  the same walk; each round of 16 K windows is counting-sorted by
+//               coarse bucket in LDS and written out in runs (whole lines) to the
+//               workgroup's segment of each bucket (straight to the lists when a
+//               bucket is one list)
+//   K3b fine    one workgroup per coarse bucket of the records with more lists than
+//               buckets: the same staged sort by list, bucket -> its lists
+//   K4 count    workgroups stride over the lists; a list (held in registers, the
+//               next one prefetched) is counted in an LDS open-addressing table
+//               (64-bit CAS claim, 32-bit add for repeats) in as many passes as keep
+//               a pass's distinct keys near 4 K (selected by hash bits 32+); each
+//               pass writes the slots it claimed, in claim order, to the list's
+//               segment and clears only those slots
 //   K5 place    exclusive scan of the distinct counts; each list's pairs are copied
 //               to their final place; records are contiguous runs of lists
-// Bytes per window: the input twice (K1, K3), an 8-byte key written and read, at
-// most 12 bytes of pairs written, read and written again.
+// Bytes per window: the input twice (K1, K3a), an 8-byte h written and read twice
+// (K3a -> K3b -> K4), 12 bytes of pairs written, read and written again.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,21 +43,38 @@
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
+#ifndef KMC_CANON_PASS
+#define KMC_CANON_PASS 4096
+#endif
+#ifndef KMC_CANON_RES
+#define KMC_CANON_RES 16
+#endif
+// Diagnostic builds only (scripts/gpu_c4_trace.sh): 1 = K4 inserts nothing, 2 = K4
+// writes no pairs.  Results are wrong.
+#ifndef KMC_CANON_ABL
+#define KMC_CANON_ABL 0
+#endif
+
 namespace kmc {
 namespace {
 
-constexpr uint64_t kEmpty = ~0ull;           // no k-mer key reaches it (62 bits at most)
-// K3 walks a piece once per group of lists, 2^KMC_CANON_SCATTER_LG groups at
-// most (write locality, see K3)
-#ifndef KMC_CANON_SCATTER_LG
-#define KMC_CANON_SCATTER_LG 2
-#endif
-constexpr int kWalkBlock = 1024;             // K1 / K3 threads per workgroup
-constexpr int kMaxLg = 14;                   // at most 16 384 lists per record (more lists: more open write segments in K3)
+constexpr uint64_t kEmptyH = 0x64B5720B4B825F21ull;  // fmix64(~0): no k-mer key (< 2^62) hashes to it
+constexpr int kWalkBlock = 1024;             // K1 / K3a / K3b threads per workgroup
+constexpr int kMaxLg = 14;                   // at most 16 384 lists per record (K1's LDS counters)
+constexpr int kCoarseLg = 7;                 // at most 128 coarse buckets per record
+constexpr int kMaxBk = 1 << kCoarseLg;       // buckets of one staged round (coarse, or lists per bucket)
 constexpr int64_t kListTarget = 4096;        // windows per list aimed at
+constexpr int kRound = 16 * kWalkBlock;      // K3a / K3b windows per staged round
 constexpr int kCountBlock = 1024;            // K4 threads per workgroup
-constexpr int kTableSlots = 12288;           // K4 LDS table: 12 288 x (8 + 4) B = 144 KB
-constexpr int kPassDistinct = 8192;          // keys per K4 pass aimed at (table load <= 2/3)
+constexpr int kTableSlots = 9216;            // K4 LDS table: 9 216 x (8 + 4) B
+constexpr int kWaves4 = kCountBlock / 64;
+constexpr int kStage = 320;                  // K4 per-wave keys staged for one probe loop
+constexpr int kClaimW = 320;                 // K4 per-wave claims per pass (2-byte slot ids)
+constexpr uint32_t kMaxInitPasses = 16;
+constexpr int kPassDistinct = KMC_CANON_PASS;  // keys per K4 pass aimed at (table load ~1/3)
+constexpr int kRes = KMC_CANON_RES;            // K4 keys per thread held in registers
+constexpr int64_t kResKeys = (int64_t)kRes * kCountBlock;
+static_assert(kPassDistinct <= kWaves4 * kClaimW && kTableSlots < 65536 , "K4 sizes");
 
 struct HParams {
     const char *data;        // global offsets (data[p] is byte p)
@@ -59,17 +83,22 @@ struct HParams {
     int64_t lo, hi;          // window starts in [lo, hi) (= [idx[0], idx[n]))
     int k;
     uint32_t flags;
-    int G;                   // K1 / K3 workgroups
+    int G;                   // K1 / K3a workgroups
     int64_t c_lo, cpw;       // chunk range start, chunks per workgroup
     const uint8_t *lg;       // [n] log2 lists of each record
     const int64_t *cbase;    // [n] cnt index of (r, list 0, its first workgroup)
+    const int64_t *ccbase;   // [n] cnt_c index of (r, coarse bucket 0, its first workgroup)
     const int32_t *w0;       // [n] first workgroup holding windows of r
     const int32_t *nwg;      // [n] workgroups holding windows of r
     const int64_t *lbase;    // [n + 1] global id of list 0 of record r (lbase[n] = lists)
     uint32_t *cnt;           // [M] windows per (record, list, workgroup)
     uint64_t *off;           // [M + 1] exclusive scan of cnt
-    uint64_t *ent;           // [windows] keys, list by list
+    uint32_t *cnt_c;         // [Mc] windows per (record, coarse bucket, workgroup)
+    uint64_t *off_c;         // [Mc + 1] exclusive scan of cnt_c
+    uint64_t *ent;           // [windows] h, list by list
+    uint64_t *ent_c;         // [windows] h, coarse bucket by bucket (K3a -> K3b; aliases pk)
     uint64_t *list_start;    // [lists + 1]
+    const int2 *fsplit;      // [K3b workgroups] (record, coarse bucket)
     uint64_t *pk;            // [windows] K4 pairs: keys
     uint32_t *pc;            // [windows] K4 pairs: counts
     uint32_t *ndist;         // [lists] distinct keys per list
@@ -85,6 +114,15 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t h) {  // MurmurHash3 finalis
     h *= 0xFF51AFD7ED558CCDull;
     h ^= h >> 33;
     h *= 0xC4CEB9FE1A85EC53ull;
+    h ^= h >> 33;
+    return h;
+}
+
+__device__ __forceinline__ uint64_t unmix64(uint64_t h) {  // inverse of fmix64
+    h ^= h >> 33;
+    h *= 0x9CB4B2F8129337DBull;
+    h ^= h >> 33;
+    h *= 0x4F74430C22A54005ull;
     h ^= h >> 33;
     return h;
 }
@@ -114,35 +152,34 @@ __device__ __forceinline__ void chunk_codes(uint4 r, bool soft, uint32_t &code, 
     bad = any ? bad_mask16(r) : 0u;
 }
 
-// Calls f(key) for every valid window of record piece [ps, pe) (window starts) of
-// a record whose terminator is at rend - 1; the workgroup's threads take the
-// piece's 16-byte chunks in turn.  Every thread runs the same number of rounds.
-template <class F>
-__device__ __forceinline__ void walk_piece(const HParams &p, int64_t ps, int64_t pe, int64_t rend, F &&f) {
+// The hashed keys of the (up to 16) valid windows starting in 16-byte chunk q of
+// record piece [ps, pe) (window starts) of a record whose terminator is at
+// rend - 1: bit j of the result is set when h[j] holds window q + j.
+__device__ __forceinline__ uint32_t chunk_keys(const HParams &p, int64_t q, int64_t ps, int64_t pe, int64_t rend,
+                                               unsigned long long (&h)[16]) {
     const int k = p.k;
     const bool soft = p.flags & KMC_CANON_SOFTMASK;
     const bool fwd_only = p.flags & KMC_CANON_FORWARD;
     const uint64_t kmask = (1ull << (2 * k)) - 1;
     const uint64_t wmask = (1ull << k) - 1;
     const int64_t hi_byte = p.idx[p.n];
-    const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
-    for (int64_t c = c0 + threadIdx.x; c < c1; c += kWalkBlock) {
-        const int64_t q = c << 4;
-        uint32_t cd[3], bd[3];
+    uint32_t cd[3], bd[3];
 #pragma unroll
-        for (int h = 0; h < 3; ++h) chunk_codes(load16(p.data, q + 16 * h, hi_byte), soft, cd[h], bd[h]);
-        const uint64_t lo64 = (uint64_t)cd[0] | ((uint64_t)cd[1] << 32);
-        const uint64_t badm = (uint64_t)bd[0] | ((uint64_t)bd[1] << 16) | ((uint64_t)bd[2] << 32);
-#pragma unroll 4
-        for (int j = 0; j < 16; ++j) {
-            const int64_t pos = q + j;
-            if (pos < ps || pos >= pe || pos > rend - 1 - k) continue;
-            if ((badm >> j) & wmask) continue;  // invalid base in the window
-            const uint64_t le = (j == 0 ? lo64 : ((lo64 >> (2 * j)) | ((uint64_t)cd[2] << (64 - 2 * j)))) & kmask;
-            const uint64_t fw = reverse_groups(le, k);
-            f(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
-        }
+    for (int i = 0; i < 3; ++i) chunk_codes(load16(p.data, q + 16 * i, hi_byte), soft, cd[i], bd[i]);
+    const uint64_t lo64 = (uint64_t)cd[0] | ((uint64_t)cd[1] << 32);
+    const uint64_t badm = (uint64_t)bd[0] | ((uint64_t)bd[1] << 16) | ((uint64_t)bd[2] << 32);
+    const int64_t last = std::min<int64_t>(pe, rend - k);  // window starts < last
+    uint32_t vm = 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int64_t pos = q + j;
+        const bool v = pos >= ps && pos < last && !((badm >> j) & wmask);
+        const uint64_t le = (j == 0 ? lo64 : ((lo64 >> (2 * j)) | ((uint64_t)cd[2] << (64 - 2 * j)))) & kmask;
+        const uint64_t fw = reverse_groups(le, k);
+        h[j] = fmix64(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
+        vm |= v ? 1u << j : 0u;
     }
+    return vm;
 }
 
 // The workgroup's chunk range and its record pieces: f(r, ps, pe, rend).
@@ -171,58 +208,135 @@ __device__ __forceinline__ void for_each_piece(const HParams &p, int64_t *s_firs
     }
 }
 
-__device__ __forceinline__ uint32_t list_of(uint64_t key, int lg) {
-    return lg ? (uint32_t)(fmix64(key) >> (64 - lg)) : 0u;
-}
+__device__ __forceinline__ int coarse_lg(int lg) { return lg < kCoarseLg ? lg : kCoarseLg; }
 
-// K1: windows per (record, list, workgroup)
+// K1: windows per (record, list, workgroup) and per (record, coarse bucket, workgroup)
 __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
     __shared__ uint32_t c[1 << kMaxLg];
     __shared__ int64_t s_first;
     const int w = blockIdx.x;
     for_each_piece(p, &s_first, [&](int64_t r, int64_t ps, int64_t pe, int64_t rend) {
-        const int lg = p.lg[r];
+        const int lg = p.lg[r], lgc = coarse_lg(lg);
         const int nb = 1 << lg;
         for (int b = threadIdx.x; b < nb; b += kWalkBlock) c[b] = 0u;
         __syncthreads();
-        walk_piece(p, ps, pe, rend, [&](uint64_t key) {
-            __hip_atomic_fetch_add(&c[list_of(key, lg)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        });
+        for (int64_t q = ((ps >> 4) + threadIdx.x) << 4; q < pe; q += (int64_t)kWalkBlock << 4) {
+            unsigned long long h[16];
+            const uint32_t vm = chunk_keys(p, q, ps, pe, rend, h);
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if ((vm >> j) & 1u)
+                    __hip_atomic_fetch_add(&c[lg ? (uint32_t)(h[j] >> (64 - lg)) : 0u], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         __syncthreads();
+        const int64_t nwg = p.nwg[r];
         const int64_t base = p.cbase[r] + (w - p.w0[r]);
-        for (int b = threadIdx.x; b < nb; b += kWalkBlock) p.cnt[base + (int64_t)b * p.nwg[r]] = c[b];
+        for (int b = threadIdx.x; b < nb; b += kWalkBlock) p.cnt[base + (int64_t)b * nwg] = c[b];
+        const int F = 1 << (lg - lgc);
+        const int64_t cbase = p.ccbase[r] + (w - p.w0[r]);
+        for (int b = threadIdx.x; b < (1 << lgc); b += kWalkBlock) {
+            uint32_t s = 0u;
+            for (int f = 0; f < F; ++f) s += c[b * F + f];
+            p.cnt_c[cbase + (int64_t)b * nwg] = s;
+        }
         __syncthreads();
     });
 }
 
-// K3: every window's key at its list position
-__global__ __launch_bounds__(kWalkBlock) void canon_scatter_kernel(HParams p) {
-    __shared__ uint32_t cur[1 << kMaxLg];  // relative to the record's first entry (< 2^32 per record)
+// One staged round of K3a / K3b: the block's (up to 16 per thread) hashes h[j]
+// (valid where bit j of vm) go to bucket bk(h) < nbk; each bucket's run is written
+// to dst at the bucket's cursor, which advances.  The round is counting-sorted in
+// LDS first, so that consecutive lanes store consecutive entries of one bucket.
+//   cnt[2][kMaxBk + 1]  bucket counts -> offsets (double-buffered by round parity)
+//   cur[kMaxBk]         global position of each bucket's next entry
+//   del[kMaxBk]         this round: global position of stage index 0 of each run
+struct Stage {
+    unsigned long long *stage;  // [kRound]
+    uint32_t (*cnt)[kMaxBk + 1];
+    unsigned long long *cur;
+    unsigned long long *del;
+};
+
+template <class Bk>
+__device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, const unsigned long long (&h)[16],
+                                             uint32_t vm, Bk bk, uint64_t *dst) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t *cn = s.cnt[par];
+    uint32_t rk[8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint32_t r = 0u;
+        if ((vm >> j) & 1u)
+            r = __hip_atomic_fetch_add(&cn[bk(h[j])], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (j & 1) rk[j >> 1] |= r << 16;
+        else rk[j >> 1] = r;
+    }
+    lds_barrier();
+    if (tid < 64) {  // exclusive scan of the nbk <= 128 counts, two per lane; cn[nbk] = total
+        const int b = 2 * lane;
+        const uint32_t a0 = b < nbk ? cn[b] : 0u, a1 = b + 1 < nbk ? cn[b + 1] : 0u;
+        const uint32_t t = a0 + a1;
+        uint32_t x = t;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (b < nbk) cn[b] = x - t;
+        if (b + 1 < nbk) cn[b + 1] = x - t + a0;
+        if (lane == 63) cn[nbk] = x;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if ((vm >> j) & 1u) s.stage[cn[bk(h[j])] + ((rk[j >> 1] >> (16 * (j & 1))) & 0xFFFFu)] = h[j];
+    for (int b = tid; b < nbk; b += kWalkBlock) {
+        const uint32_t o0 = cn[b], o1 = cn[b + 1];
+        const unsigned long long g = s.cur[b];
+        s.del[b] = g - o0;
+        s.cur[b] = g + (o1 - o0);
+    }
+    const uint32_t total = cn[nbk];
+    uint32_t *nx = s.cnt[par ^ 1];  // next round's counts (last read before this round's first barrier)
+    for (int b = tid; b <= nbk; b += kWalkBlock) nx[b] = 0u;
+    lds_barrier();
+    for (uint32_t i = tid; i < total; i += kWalkBlock) {
+        const unsigned long long x = s.stage[i];
+        dst[s.del[bk(x)] + i] = x;
+    }
+    // the next round writes stage / del only after two barriers, which every
+    // thread reaches after this write-out
+}
+
+// K3a: every window's h at its coarse bucket's position (ent_c), or at its list
+// position (ent) for records whose buckets are single lists
+__global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
+    __shared__ unsigned long long s_stage[kRound];
+    __shared__ uint32_t s_cnt[2][kMaxBk + 1];
+    __shared__ unsigned long long s_cur[kMaxBk], s_del[kMaxBk];
     __shared__ int64_t s_first;
+    const Stage st{s_stage, s_cnt, s_cur, s_del};
     const int w = blockIdx.x;
+    int par = 0;
     for_each_piece(p, &s_first, [&](int64_t r, int64_t ps, int64_t pe, int64_t rend) {
-        const int lg = p.lg[r];
-        const int nb = 1 << lg;
-        const int64_t base = p.cbase[r] + (w - p.w0[r]);
-        const uint64_t rbase = p.off[p.cbase[r]];
-        for (int b = threadIdx.x; b < nb; b += kWalkBlock)
-            cur[b] = (uint32_t)(p.off[base + (int64_t)b * p.nwg[r]] - rbase);
+        const int lg = p.lg[r], lgc = coarse_lg(lg);
+        const int nbk = 1 << lgc;
+        const int64_t nwg = p.nwg[r];
+        const int64_t base = p.ccbase[r] + (w - p.w0[r]);
+        for (int b = threadIdx.x; b < nbk; b += kWalkBlock) s_cur[b] = p.off_c[base + (int64_t)b * nwg];
+        for (int b = threadIdx.x; b < 2 * (kMaxBk + 1); b += kWalkBlock) (&s_cnt[0][0])[b] = 0u;
         __syncthreads();
-        uint64_t *ent = p.ent + rbase;
-        // the piece is walked once per group of lists: a workgroup keeps one
-        // partially written 128-B line open per list it writes, and with all of a
-        // record's lists open on every workgroup those lines overflow the
-        // Infinity Cache, turning each 8-B key store into a read-modify-write in HBM
-        const int glg = lg < KMC_CANON_SCATTER_LG ? lg : KMC_CANON_SCATTER_LG;  // log2 groups
-        const int gshift = lg - glg;
-        const uint32_t ng = 1u << glg;
-        for (uint32_t g = 0; g < ng; ++g) {
-            walk_piece(p, ps, pe, rend, [&](uint64_t key) {
-                const uint32_t l = list_of(key, lg);
-                if ((l >> gshift) != g) return;
-                const uint32_t i = __hip_atomic_fetch_add(&cur[l], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                ent[i] = key;
-            });
+        uint64_t *dst = lg > lgc ? p.ent_c : p.ent;
+        const auto bk = [lgc](unsigned long long x) { return lgc ? (uint32_t)(x >> (64 - lgc)) : 0u; };
+        const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
+        for (int64_t cb = c0; cb < c1; cb += kWalkBlock) {
+            const int64_t c = cb + threadIdx.x;
+            unsigned long long h[16];
+            uint32_t vm = 0u;
+            if (c < c1) vm = chunk_keys(p, c << 4, ps, pe, rend, h);
+            staged_round(st, par, nbk, h, vm, bk, dst);
+            par ^= 1;
         }
         __syncthreads();
     });
@@ -245,102 +359,245 @@ __global__ void canon_list_start_kernel(HParams p) {
     p.list_start[l] = p.off[p.cbase[a] + (l - p.lbase[a]) * p.nwg[a]];
 }
 
-// K4: one workgroup per list.  Pass q of P counts the keys whose hash bits
-// [32, 32 + log2 P) equal q; a pass whose keys overflow the table is split again.
-__global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
-    __shared__ unsigned long long tk[kTableSlots];
-    __shared__ uint32_t tc[kTableSlots];
-    __shared__ uint32_t s_misc[4 + kCountBlock / 64];
-    const int64_t l = blockIdx.x;
-    const uint64_t beg = p.list_start[l], end = p.list_start[l + 1];
-    const uint64_t n = end - beg;
-    uint32_t P = 1;
-    while ((uint64_t)P * kPassDistinct < n) P <<= 1;
-    uint64_t out = beg;  // next free pair of this list's segment
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (uint32_t q = 0; q < P;) {
-        for (int i = tid; i < kTableSlots; i += kCountBlock) {
-            tk[i] = kEmpty;
-            tc[i] = 0u;
+// K3b: one workgroup per coarse bucket of a record with several lists per bucket;
+// the bucket's entries (ent_c) to its lists (ent)
+__global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
+    __shared__ unsigned long long s_stage[kRound];
+    __shared__ uint32_t s_cnt[2][kMaxBk + 1];
+    __shared__ unsigned long long s_cur[kMaxBk], s_del[kMaxBk];
+    const Stage st{s_stage, s_cnt, s_cur, s_del};
+    const int2 rc = p.fsplit[blockIdx.x];
+    const int lg = p.lg[rc.x], lgc = coarse_lg(lg);
+    const int F = 1 << (lg - lgc);
+    const int64_t lb = p.lbase[rc.x] + (int64_t)rc.y * F;
+    const uint64_t a0 = p.list_start[lb], a1 = p.list_start[lb + F];
+    for (int f = threadIdx.x; f < F; f += kWalkBlock) s_cur[f] = p.list_start[lb + f];
+    for (int b = threadIdx.x; b < 2 * (kMaxBk + 1); b += kWalkBlock) (&s_cnt[0][0])[b] = 0u;
+    __syncthreads();
+    const auto bk = [lg, F](unsigned long long x) { return (uint32_t)(x >> (64 - lg)) & (uint32_t)(F - 1); };
+    int par = 0;
+    for (uint64_t i0 = a0; i0 < a1; i0 += kRound) {
+        unsigned long long h[16];
+        uint32_t vm = 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
+            h[j] = i < a1 ? p.ent_c[i] : 0ull;
+            vm |= i < a1 ? 1u << j : 0u;
         }
-        if (tid == 0) s_misc[0] = 0u;  // overflow flag
-        __syncthreads();
-        const uint32_t lgP = 31 - __builtin_clz(P);
-        // the list in batches of kBatch keys per thread: all loads of a batch are in
-        // flight together (one HBM latency per batch, not per key)
-        constexpr int kBatch = 8;
-        for (uint64_t i0 = beg; i0 < end; i0 += (uint64_t)kBatch * kCountBlock) {
-            unsigned long long kb[kBatch];
+        staged_round(st, par, F, h, vm, bk, p.ent);
+        par ^= 1;
+    }
+}
+
+// K4: lists counted in an LDS table, workgroups striding over the lists.  Its
+// barriers are LDS-only (lds_barrier): __syncthreads would also wait for the pair
+// stores and for the next list's key prefetch.
+//
+// An LDS 64-bit CAS costs the LDS ~21 cycles per wave instruction however few
+// lanes are active (scripts/lds_microbench.hip, modes 14/16), so the probe loop
+// keeps every lane busy: each wave stages its keys of the pass in a private LDS
+// queue and its lanes take queue entries as they finish their probe chains.
+// Each wave lists the slots its lanes claimed, so that the write-out and the
+// table clear touch only the pass's distinct keys.
+__device__ __forceinline__ void load_keys(const uint64_t *ent, uint64_t i0, uint64_t end,
+                                          unsigned long long (&kh)[kRes]) {
 #pragma unroll
-            for (int j = 0; j < kBatch; ++j) {
-                const uint64_t i = i0 + (uint64_t)j * kCountBlock + tid;
-                kb[j] = i < end ? p.ent[i] : kEmpty;
+    for (int j = 0; j < kRes; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * kCountBlock + threadIdx.x;
+        kh[j] = i < end ? ent[i] : kEmptyH;
+    }
+}
+
+struct K4Lds {
+    unsigned long long tk[kTableSlots];          // slot keys (h), kEmptyH when free
+    uint32_t tc[kTableSlots];                    // slot occurrences - 1
+    unsigned long long qk[kWaves4][kStage];      // per wave: keys being inserted
+    uint16_t cl[kWaves4][kClaimW];               // per wave: slots claimed this pass
+    uint32_t ncl[2][kWaves4];                    // per wave: claims (by pass parity)
+    uint32_t ovf[2];                             // pass overflow flags (by pass parity)
+};
+
+// Inserts the nq keys staged in qk[wv]: a lane without a key takes the next one.
+// The slots its lanes claim are appended to cl[wv] (ncl: wave-uniform count).  Sets
+// *ovf when the claim list or the table is full (more distinct keys than the pass
+// allows: splitting the pass helps, unlike for repeats, which never claim).
+__device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint32_t *ovf, uint32_t &ncl) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const unsigned long long *qk = L.qk[wv];
+    uint16_t *cl = L.cl[wv];
+    uint32_t cursor = 0;
+    bool busy = false;
+    unsigned long long h = 0;
+    uint32_t s = 0, probes = 0;
+    for (;;) {
+        const uint64_t mn = __ballot(!busy);
+        if (!busy) {
+            const uint32_t at = cursor + (uint32_t)__popcll(mn & lt);
+            if (at < nq) {
+                busy = true;
+                h = qk[at];
+                s = (uint32_t)(((h & 0xFFFFFFFFull) * (uint64_t)kTableSlots) >> 32);
+                probes = 0;
             }
-#pragma unroll
-            for (int j = 0; j < kBatch; ++j) {
-                const unsigned long long key = kb[j];
-                if (key == kEmpty) continue;
-                const uint64_t h = fmix64(key);
-                if (lgP && (uint32_t)((h >> 32) & (P - 1)) != q) continue;
-                uint32_t s = (uint32_t)(((h & 0xFFFFFFFFull) * kTableSlots) >> 32);
-                uint32_t probes = 0;
-                for (;;) {
-                    const unsigned long long cur = atomicCAS(&tk[s], kEmpty, key);
-                    if (cur == kEmpty) break;  // claimed: first occurrence (tc holds occurrences - 1)
-                    if (cur == key) {
-                        __hip_atomic_fetch_add(&tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        break;
-                    }
-                    if (++probes == kTableSlots) {  // table full: this pass splits in two
-                        s_misc[0] = 1u;
-                        break;
-                    }
-                    s = s + 1 == (uint32_t)kTableSlots ? 0u : s + 1;
+        }
+        cursor += (uint32_t)__popcll(mn);
+        if (!__ballot(busy)) break;
+        bool claimed = false;
+        if (busy) {
+            unsigned long long cur = kEmptyH;
+            __hip_atomic_compare_exchange_strong(&L.tk[s], &cur, h, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur == kEmptyH) {  // first occurrence (tc holds occurrences - 1)
+                claimed = true;
+                busy = false;
+            } else if (cur == h) {
+                __hip_atomic_fetch_add(&L.tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                busy = false;
+            } else {
+                s = s + 1 == (uint32_t)kTableSlots ? 0u : s + 1;
+                if (++probes == (uint32_t)kTableSlots) {  // table full
+                    *ovf = 1u;
+                    busy = false;
                 }
             }
         }
-        __syncthreads();
-        if (s_misc[0]) {
-            // restart with twice the passes (pass q -> passes 2q, 2q+1); the pairs of
-            // the passes already written stay, since the pass split refines them
-            __syncthreads();
-            P <<= 1;
-            q <<= 1;
-            continue;
+        const uint64_t mc = __ballot(claimed);
+        if (claimed) {
+            const uint32_t at = ncl + (uint32_t)__popcll(mc & lt);
+            if (at < (uint32_t)kClaimW) cl[at] = (uint16_t)s;
+            else *ovf = 1u;
         }
-        // compact the live slots to the list's segment, slot order
-        constexpr int PER = kTableSlots / kCountBlock;
-        uint32_t live = 0;
+        ncl += (uint32_t)__popcll(mc);
+    }
+}
+
+// The wave's keys of pass q / P, staged in its LDS queue and probed; a queue that
+// fills up (repeats beyond the pass target) is probed and refilled.
+__device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes], uint32_t q, uint32_t P, K4Lds &L,
+                                            int wv, uint32_t *ovf, uint32_t &ncl) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    unsigned long long *qk = L.qk[wv];
+    int next = 0;  // first key slot not yet staged (wave-uniform)
+    do {
+        uint32_t nq = 0;  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < PER; ++j) live += tk[tid * PER + j] != kEmpty;
-        uint32_t x = live;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_misc[4 + wid] = x;
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (int i2 = 0; i2 < kCountBlock / 64; ++i2) {
-            if (i2 < wid) before += s_misc[4 + i2];
-            total += s_misc[4 + i2];
-        }
-        uint64_t o2 = out + before + x - live;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const unsigned long long key = tk[tid * PER + j];
-            if (key != kEmpty) {
-                p.pk[o2] = key;
-                p.pc[o2] = tc[tid * PER + j] + 1u;
-                ++o2;
+        for (int j = 0; j < kRes; ++j) {
+            if (j >= next && nq <= (uint32_t)(kStage - 64)) {
+                const unsigned long long h = kh[j];
+                const bool in = h != kEmptyH && ((uint32_t)(h >> 32) & (P - 1u)) == q;
+                const uint64_t m = __ballot(in);
+                if (in) qk[nq + (uint32_t)__popcll(m & lt)] = h;
+                nq += (uint32_t)__popcll(m);
+                next = j + 1;
             }
         }
-        out += total;
-        __syncthreads();
-        ++q;
+        if (nq) probe_staged(L, wv, nq, ovf, ncl);
+    } while (next < kRes);
+}
+
+__global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
+    __shared__ K4Lds L;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int i = tid; i < kTableSlots; i += kCountBlock) {
+        L.tk[i] = kEmptyH;
+        L.tc[i] = 0u;
     }
-    if (tid == 0) p.ndist[l] = (uint32_t)(out - beg);
+    if (tid < 2) L.ovf[tid] = 0u;
+    lds_barrier();
+    const int64_t G = gridDim.x;
+    int64_t l = blockIdx.x;
+    if (l >= p.lists) return;
+    // list bounds two lists ahead, keys one list ahead
+    uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1], b1 = 0, e1 = 0;
+    if (l + G < p.lists) {
+        b1 = p.list_start[l + G];
+        e1 = p.list_start[l + G + 1];
+    }
+    unsigned long long kr[kRes], kn[kRes];
+    if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
+    int par = 0;
+    for (; l < p.lists; l += G) {
+        uint64_t b2 = 0, e2 = 0;
+        if (l + 2 * G < p.lists) {
+            b2 = p.list_start[l + 2 * G];
+            e2 = p.list_start[l + 2 * G + 1];
+        }
+        if (l + G < p.lists && e1 - b1 <= (uint64_t)kResKeys) load_keys(p.ent, b1, e1, kn);
+        const uint64_t n = e0 - b0;
+        const bool resident = n <= (uint64_t)kResKeys;
+        // passes from the list length, capped: repeats do not need passes, and a
+        // pass with too many distinct keys overflows and splits
+        uint32_t P = 1;
+        while ((uint64_t)P * kPassDistinct < n && P < kMaxInitPasses) P <<= 1;
+        uint64_t out = b0;  // next free pair of this list's segment
+        for (uint32_t q = 0; q < P;) {
+            uint32_t ncl = 0;
+            if (resident) {
+                wave_insert(kr, q, P, L, wv, &L.ovf[par], ncl);
+            } else {
+                for (uint64_t i0 = b0; i0 < e0; i0 += (uint64_t)kResKeys) {
+                    load_keys(p.ent, i0, e0, kr);
+                    wave_insert(kr, q, P, L, wv, &L.ovf[par], ncl);
+                }
+            }
+            if (lane == 0) L.ncl[par][wv] = ncl;
+            lds_barrier();
+            const bool ovf = L.ovf[par] != 0u;
+            if (tid == 0) L.ovf[par ^ 1] = 0u;  // last read before this barrier
+            if (ovf) {
+                // clear the table and redo with twice the passes (pass q -> passes 2q,
+                // 2q+1); the pairs of the passes already written stay, the split refines
+                for (int i = tid; i < kTableSlots; i += kCountBlock) {
+                    L.tk[i] = kEmptyH;
+                    L.tc[i] = 0u;
+                }
+                lds_barrier();
+                P <<= 1;
+                q <<= 1;
+                par ^= 1;
+                continue;
+            }
+            uint32_t before = 0, total = 0;
+#pragma unroll
+            for (int w2 = 0; w2 < kWaves4; ++w2) {
+                const uint32_t v = L.ncl[par][w2];
+                before += w2 < wv ? v : 0u;
+                total += v;
+            }
+            // the wave's claimed slots, in claim order (coalesced), cleared
+            const uint16_t *cl = L.cl[wv];
+            for (uint32_t i = lane; i < ncl; i += 64) {
+                const uint32_t sl = cl[i];
+                const unsigned long long h = L.tk[sl];
+                const uint32_t c = L.tc[sl];
+                L.tk[sl] = kEmptyH;
+                L.tc[sl] = 0u;
+#if KMC_CANON_ABL == 2
+                if (c == 0xFFFFFFF0u)
+#endif
+                {
+                    p.pk[out + before + i] = unmix64(h);
+                    p.pc[out + before + i] = c + 1u;
+                }
+            }
+            out += total;
+            lds_barrier();
+            par ^= 1;
+            ++q;
+        }
+        if (tid == 0) p.ndist[l] = (uint32_t)(out - b0);
+#pragma unroll
+        for (int j = 0; j < kRes; ++j) kr[j] = kn[j];
+        b0 = b1;
+        e0 = e1;
+        b1 = b2;
+        e1 = e2;
+    }
 }
 
 // K5: pairs to their final place; record offsets
@@ -394,7 +651,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     int device = 0, cus = 0;
     if ((he = hipGetDevice(&device)) || (he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)))
         return (int)he;
-    // geometry of K1 / K3: G workgroups over the window chunks
+    // geometry of K1 / K3a: G workgroups over the window chunks
     HParams p{};
     p.data = data;
     p.idx = indices;
@@ -407,16 +664,19 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     const int64_t chunks = p.hi > p.lo ? ((p.hi + 15) >> 4) - p.c_lo : 0;
     p.G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, chunks));
     p.cpw = std::max<int64_t>(1, (chunks + p.G - 1) / p.G);
-    // per record: lists, workgroups holding its windows, cnt layout, list ids
+    // per record: lists, coarse buckets, workgroups holding its windows, cnt
+    // layouts, list ids, K3b workgroups
     std::vector<uint8_t> lg(n);
     std::vector<int32_t> w0(n), nwg(n);
-    std::vector<int64_t> cbase(n + 1), lbase(n + 1);
-    int64_t M = 0, L = 0, windows = 0;
+    std::vector<int64_t> cbase(n + 1), ccbase(n + 1), lbase(n + 1);
+    std::vector<int2> fsplit;
+    int64_t M = 0, Mc = 0, L = 0, windows = 0;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t a = hidx[r], nw = std::max<int64_t>(0, hidx[r + 1] - a - k);
         windows += nw;
         int g = 0;
         while (g < kMaxLg && ((int64_t)kListTarget << g) < nw) ++g;
+        const int gc = g < kCoarseLg ? g : kCoarseLg;
         lg[r] = (uint8_t)g;
         if (nw > 0) {
             const int64_t cf = a >> 4, cl = (a + nw - 1) >> 4;
@@ -427,23 +687,33 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
             nwg[r] = 0;
         }
         cbase[r] = M;
+        ccbase[r] = Mc;
         lbase[r] = L;
         M += ((int64_t)1 << g) * nwg[r];
+        Mc += ((int64_t)1 << gc) * nwg[r];
         L += (int64_t)1 << g;
+        if (g > gc && nw > 0)
+            for (int c = 0; c < (1 << gc); ++c) fsplit.push_back(make_int2((int)r, c));
     }
     cbase[n] = M;
+    ccbase[n] = Mc;
     lbase[n] = L;
     p.lists = L;
+    const int64_t NF = (int64_t)fsplit.size();
     const int64_t cap_w = std::max<int64_t>(windows, 1);
     // workspace
     size_t o = 0;
     const size_t o_lg = o; o += al256(n);
     const size_t o_cb = o; o += al256((n + 1) * 8);
+    const size_t o_ccb = o; o += al256((n + 1) * 8);
     const size_t o_w0 = o; o += al256(n * 4);
     const size_t o_nw = o; o += al256(n * 4);
     const size_t o_lb = o; o += al256((n + 1) * 8);
+    const size_t o_fs = o; o += al256((size_t)std::max<int64_t>(NF, 1) * sizeof(int2));
     const size_t o_cnt = o; o += al256((size_t)std::max<int64_t>(M, 1) * 4);
     const size_t o_off = o; o += al256((size_t)(M + 1) * 8);
+    const size_t o_cntc = o; o += al256((size_t)std::max<int64_t>(Mc, 1) * 4);
+    const size_t o_offc = o; o += al256((size_t)(Mc + 1) * 8);
     const size_t o_bs = o; o += al256((size_t)(scan_tiles(std::max<int64_t>(M, L)) + 1) * 8);
     const size_t o_ent = o; o += al256((size_t)cap_w * 8);
     const size_t o_ls = o; o += al256((size_t)(L + 1) * 8);
@@ -468,15 +738,20 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     }
     p.lg = reinterpret_cast<uint8_t *>(ws + o_lg);
     p.cbase = reinterpret_cast<int64_t *>(ws + o_cb);
+    p.ccbase = reinterpret_cast<int64_t *>(ws + o_ccb);
     p.w0 = reinterpret_cast<int32_t *>(ws + o_w0);
     p.nwg = reinterpret_cast<int32_t *>(ws + o_nw);
     p.lbase = reinterpret_cast<int64_t *>(ws + o_lb);
+    p.fsplit = reinterpret_cast<int2 *>(ws + o_fs);
     p.cnt = reinterpret_cast<uint32_t *>(ws + o_cnt);
     p.off = reinterpret_cast<uint64_t *>(ws + o_off);
+    p.cnt_c = reinterpret_cast<uint32_t *>(ws + o_cntc);
+    p.off_c = reinterpret_cast<uint64_t *>(ws + o_offc);
     uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + o_bs);
     p.ent = reinterpret_cast<uint64_t *>(ws + o_ent);
     p.list_start = reinterpret_cast<uint64_t *>(ws + o_ls);
     p.pk = reinterpret_cast<uint64_t *>(ws + o_pk);
+    p.ent_c = p.pk;  // dead before K4 writes the pairs
     p.pc = reinterpret_cast<uint32_t *>(ws + o_pc);
     p.ndist = reinterpret_cast<uint32_t *>(ws + o_nd);
     p.dist_off = reinterpret_cast<uint64_t *>(ws + o_do);
@@ -485,18 +760,27 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     p.out_counts = counts;
     if ((he = hipMemcpyAsync((void *)p.lg, lg.data(), n, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.cbase, cbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
+        (he = hipMemcpyAsync((void *)p.ccbase, ccbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.w0, w0.data(), n * 4, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.nwg, nwg.data(), n * 4, hipMemcpyHostToDevice, stream)) ||
-        (he = hipMemcpyAsync((void *)p.lbase, lbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)))
+        (he = hipMemcpyAsync((void *)p.lbase, lbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
+        (NF && (he = hipMemcpyAsync((void *)p.fsplit, fsplit.data(), NF * sizeof(int2), hipMemcpyHostToDevice,
+                                    stream))))
         return (int)he;
     if (M > 0) {
-        if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream))) return (int)he;
+        if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream)) ||
+            (he = hipMemsetAsync(p.cnt_c, 0, (size_t)Mc * 4, stream)))
+            return (int)he;
         hipLaunchKernelGGL(canon_count_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
     }
     excl_scan_u32(p.cnt, M, bsum, p.off, stream);
-    hipLaunchKernelGGL(canon_scatter_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
+    excl_scan_u32(p.cnt_c, Mc, bsum, p.off_c, stream);
+    hipLaunchKernelGGL(canon_coarse_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
     hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
-    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)L), dim3(kCountBlock), 0, stream, p);
+    if (NF > 0) hipLaunchKernelGGL(canon_fine_kernel, dim3((unsigned)NF), dim3(kWalkBlock), 0, stream, p);
+    // persistent: one workgroup per CU (the table fills its LDS) striding over the lists
+    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, cus))),
+                       dim3(kCountBlock), 0, stream, p);
     excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);
     hipLaunchKernelGGL(canon_recoff_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
     uint64_t distinct = 0;

@@ -16,6 +16,12 @@
 //   mode 11 ds_add_u32, random word of 8 192, 4 replicas interleaved by lane % 4
 //   mode 12 ds_add_u32, random word of 32 768, replica-free, but only lanes 0-31 active
 //   mode 13 ds_add_u64, random qword of 8 192, 2 replicas interleaved by lane parity
+//   mode 14 ds_cmpst_rtn_b64, random qword of 16 384 (the compare never matches: no store)
+//   mode 15 ds_cmpst_rtn_b64, conflict-free (lane -> its own qword)
+//   mode 16 ds_cmpst_rtn_b64, random, only lanes 0-15 active
+//   mode 17 ds_cmpst_rtn_b32, random word of 32 768
+//   mode 18 ds_read_b64, random qword of 16 384
+//   mode 19 ds_cmpst_rtn_b64, random, one wait per op (dependent chain: latency)
 // Build: hipcc --offload-arch=gfx950 -O3 -o lds_microbench scripts/lds_microbench.hip
 // Run:   ./lds_microbench      (one JSON line per mode)
 #include <hip/hip_runtime.h>
@@ -95,6 +101,35 @@ __global__ __launch_bounds__(BLOCK) void lds_kernel(int iters, uint32_t *out) {
             } else if constexpr (MODE == 13) {
                 __hip_atomic_fetch_add(&h64[((r & 0x1FFFu) << 1) | (lane & 1)], 0x0000000100000001ull,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if constexpr (MODE == 14) {
+                uint64_t c = 1ull;  // the table holds even values only
+                __hip_atomic_compare_exchange_strong(&h64[r & 0x3FFFu], &c, 3ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                acc += (uint32_t)c;
+            } else if constexpr (MODE == 15) {
+                uint64_t c = 1ull;
+                __hip_atomic_compare_exchange_strong(&h64[((r & 0xFFu) << 6) | lane], &c, 3ull, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                acc += (uint32_t)c;
+            } else if constexpr (MODE == 16) {
+                if (lane < 16) {
+                    uint64_t c = 1ull;
+                    __hip_atomic_compare_exchange_strong(&h64[r & 0x3FFFu], &c, 3ull, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    acc += (uint32_t)c;
+                }
+            } else if constexpr (MODE == 17) {
+                uint32_t c = 1u;
+                __hip_atomic_compare_exchange_strong(&h[r & 0x7FFFu], &c, 3u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                acc += c;
+            } else if constexpr (MODE == 18) {
+                acc += (uint32_t)__hip_atomic_load(&h64[r & 0x3FFFu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if constexpr (MODE == 19) {
+                uint64_t c = 1ull;
+                __hip_atomic_compare_exchange_strong(&h64[(r ^ acc) & 0x3FFFu], &c, 3ull, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                acc += (uint32_t)c;
             } else if constexpr (MODE == 9) {
                 __hip_atomic_fetch_add(&h[((r & 0x3FFu) << 5) | ((lane & 31) >> 1)], 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -157,6 +192,12 @@ int main() {
     r |= run<11>(cus, iters, out, "add_u32 random, 4 replicas by lane%4");
     r |= run<12>(cus, iters, out, "add_u32 random, lanes 0-31 only");
     r |= run<13>(cus, iters, out, "add_u64 random, 2 replicas by lane parity");
+    r |= run<14>(cus, iters, out, "cmpst_rtn_b64 random (no store)");
+    r |= run<15>(cus, iters, out, "cmpst_rtn_b64 conflict-free");
+    r |= run<16>(cus, iters, out, "cmpst_rtn_b64 random, 16 lanes");
+    r |= run<17>(cus, iters, out, "cmpst_rtn_b32 random");
+    r |= run<18>(cus, iters, out, "read_b64 random");
+    r |= run<19>(cus, iters, out, "cmpst_rtn_b64 random, dependent chain");
     CHECK(hipFree(out));
     return r;
 }

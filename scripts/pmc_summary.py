@@ -10,6 +10,7 @@ from collections import defaultdict
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     m = re.search(r"(\w+)<([^>]*)>", name)
     if m:
         return "%s<%s>" % (m.group(1), m.group(2).replace("(anonymous namespace)::", ""))
