@@ -44,7 +44,7 @@
 #include "kmc_stream.h"
 
 #ifndef KMC_CANON_PASS
-#define KMC_CANON_PASS 4096
+#define KMC_CANON_PASS 2048
 #endif
 #ifndef KMC_CANON_RES
 #define KMC_CANON_RES 16
@@ -60,18 +60,24 @@ namespace {
 
 constexpr uint64_t kEmptyH = 0x64B5720B4B825F21ull;  // fmix64(~0): no k-mer key (< 2^62) hashes to it
 constexpr int kWalkBlock = 1024;             // K1 / K3a / K3b threads per workgroup
-constexpr int kMaxLg = 14;                   // at most 16 384 lists per record (K1's LDS counters)
+constexpr int kMaxLg = 15;                   // at most 32 768 lists per record (K1's LDS counters)
 constexpr int kCoarseLg = 7;                 // at most 128 coarse buckets per record
-constexpr int kMaxBk = 1 << kCoarseLg;       // buckets of one staged round (coarse, or lists per bucket)
+constexpr int kMaxBk = 1 << (kMaxLg - kCoarseLg);  // buckets of one staged round (coarse, or lists per bucket)
 constexpr int64_t kListTarget = 4096;        // windows per list aimed at
 constexpr int kRound = 16 * kWalkBlock;      // K3a / K3b windows per staged round
-constexpr int kCountBlock = 1024;            // K4 threads per workgroup
-constexpr int kTableSlots = 9216;            // K4 LDS table: 9 216 x (8 + 4) B
+constexpr int kCountBlock = 512;             // K4 threads per workgroup (two workgroups per CU)
+constexpr int kTableLg = 12;
+constexpr int kTableSlots = 1 << kTableLg;   // K4 LDS table: 4 096 x (8 + 4) B, double hashing
 constexpr int kWaves4 = kCountBlock / 64;
-constexpr int kStage = 320;                  // K4 per-wave keys staged for one probe loop
+#ifndef KMC_CANON_STAGE
+#define KMC_CANON_STAGE 256
+#endif
+constexpr int kStage = KMC_CANON_STAGE;                // K4 per-wave keys staged for one probe loop
 constexpr int kClaimW = 320;                 // K4 per-wave claims per pass (2-byte slot ids)
 constexpr uint32_t kMaxInitPasses = 16;
-constexpr int kPassDistinct = KMC_CANON_PASS;  // keys per K4 pass aimed at (table load ~1/3)
+constexpr int kPassTop = 64 - kMaxLg;          // pass bits [kPassTop - log2 P, kPassTop), below the list bits
+constexpr uint32_t kMaxPasses = 1u << (kPassTop - 32);
+constexpr int kPassDistinct = KMC_CANON_PASS;  // keys per K4 pass aimed at (table load <= 0.47)
 constexpr int kRes = KMC_CANON_RES;            // K4 keys per thread held in registers
 constexpr int64_t kResKeys = (int64_t)kRes * kCountBlock;
 static_assert(kPassDistinct <= kWaves4 * kClaimW && kTableSlots < 65536 , "K4 sizes");
@@ -104,6 +110,8 @@ struct HParams {
     uint32_t *ndist;         // [lists] distinct keys per list
     uint64_t *dist_off;      // [lists + 1] exclusive scan of ndist
     int64_t lists;
+    uint32_t *err;           // set when a list exceeds what K4 can split
+    uint32_t claim_cap;      // K4 claims per wave and pass (kClaimW; smaller only in tests)
     uint64_t *rec_off;       // [n + 1] output offsets
     uint64_t *out_keys;
     uint32_t *out_counts;
@@ -273,18 +281,27 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
         else rk[j >> 1] = r;
     }
     lds_barrier();
-    if (tid < 64) {  // exclusive scan of the nbk <= 128 counts, two per lane; cn[nbk] = total
-        const int b = 2 * lane;
-        const uint32_t a0 = b < nbk ? cn[b] : 0u, a1 = b + 1 < nbk ? cn[b + 1] : 0u;
-        const uint32_t t = a0 + a1;
+    if (tid < 64) {  // exclusive scan of the nbk <= kMaxBk counts, kPerLane per lane; cn[nbk] = total
+        constexpr int kPerLane = kMaxBk / 64;
+        const int b = kPerLane * lane;
+        uint32_t a[kPerLane], t = 0u;
+#pragma unroll
+        for (int i = 0; i < kPerLane; ++i) {
+            a[i] = b + i < nbk ? cn[b + i] : 0u;
+            t += a[i];
+        }
         uint32_t x = t;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(x, o);
             if (lane >= o) x += y;
         }
-        if (b < nbk) cn[b] = x - t;
-        if (b + 1 < nbk) cn[b + 1] = x - t + a0;
+        uint32_t run = x - t;
+#pragma unroll
+        for (int i = 0; i < kPerLane; ++i) {
+            if (b + i < nbk) cn[b + i] = run;
+            run += a[i];
+        }
         if (lane == 63) cn[nbk] = x;
     }
     lds_barrier();
@@ -413,70 +430,105 @@ struct K4Lds {
     unsigned long long tk[kTableSlots];          // slot keys (h), kEmptyH when free
     uint32_t tc[kTableSlots];                    // slot occurrences - 1
     unsigned long long qk[kWaves4][kStage];      // per wave: keys being inserted
-    uint16_t cl[kWaves4][kClaimW];               // per wave: slots claimed this pass
+    uint16_t cl[kWaves4][kClaimW + 1];           // per wave: slots claimed this pass (+ a spare entry)
     uint32_t ncl[2][kWaves4];                    // per wave: claims (by pass parity)
     uint32_t ovf[2];                             // pass overflow flags (by pass parity)
+    unsigned long long dummy[64];                // per lane: CAS target of an idle lane
 };
 
-// Inserts the nq keys staged in qk[wv]: a lane without a key takes the next one.
-// The slots its lanes claim are appended to cl[wv] (ncl: wave-uniform count).  Sets
-// *ovf when the claim list or the table is full (more distinct keys than the pass
-// allows: splitting the pass helps, unlike for repeats, which never claim).
-__device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint32_t *ovf, uint32_t &ncl) {
+#ifdef KMC_CANON_PROF
+__device__ unsigned long long g_prof2[4];  // probe rounds, staged keys, probe loops
+#endif
+// LDS byte offset of a __shared__ object
+template <class T>
+__device__ __forceinline__ uint32_t lds_off(T *p) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T *)p;
+}
+
+// ds_cmpst_rtn_b64: the old value at LDS byte offset off (stores val if it was cmp)
+__device__ __forceinline__ unsigned long long lds_cas64(uint32_t off, unsigned long long cmp,
+                                                        unsigned long long val) {
+    unsigned long long old;
+    asm volatile("ds_cmpst_rtn_b64 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(old) : "v"(off), "v"(cmp), "v"(val) : "memory");
+    return old;
+}
+
+// Inserts the nq keys staged in qk[wv]: a lane without a key takes the next one,
+// so the wave's CAS instructions stay full until the queue drains (an LDS CAS
+// costs the same however few lanes are active).  The loop body is branch-free
+// but for repeats: an idle lane's CAS goes to its dummy slot (never kEmptyH, so
+// it fails), its claim record to the spare entry.  The slots claimed are appended
+// to cl[wv] (ncl: wave-uniform count); a wave that claims more than kClaimW
+// raises *ovf and stops (the pass is redone split in two), which also bounds the
+// table's load below one: no probe chain can wrap.
+__device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint32_t cap, uint32_t *ovf,
+                                             uint32_t &ncl) {
+#ifdef KMC_CANON_PROF
+    uint32_t rounds = 0;
+#endif
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     const unsigned long long *qk = L.qk[wv];
     uint16_t *cl = L.cl[wv];
+    const uint32_t tk0 = lds_off(&L.tk[0]), dummy = lds_off(&L.dummy[lane]);
+    if (ncl > cap) return;  // this pass already overflowed
     uint32_t cursor = 0;
     bool busy = false;
     unsigned long long h = 0;
-    uint32_t s = 0, probes = 0;
+    uint32_t s = 0, step = 1;
     for (;;) {
         const uint64_t mn = __ballot(!busy);
-        if (!busy) {
-            const uint32_t at = cursor + (uint32_t)__popcll(mn & lt);
-            if (at < nq) {
-                busy = true;
-                h = qk[at];
-                s = (uint32_t)(((h & 0xFFFFFFFFull) * (uint64_t)kTableSlots) >> 32);
-                probes = 0;
-            }
-        }
+        const uint32_t at = cursor + (uint32_t)__popcll(mn & lt);
         cursor += (uint32_t)__popcll(mn);
+        const bool take = !busy && at < nq;
+        const unsigned long long nk = qk[take ? at : 0u];
+        h = take ? nk : h;
+        s = take ? ((uint32_t)nk & (kTableSlots - 1)) : s;
+        step = take ? (((uint32_t)(nk >> kTableLg) & (kTableSlots - 1)) | 1u) : step;  // odd: visits every slot
+        busy = busy || take;
         if (!__ballot(busy)) break;
-        bool claimed = false;
-        if (busy) {
-            unsigned long long cur = kEmptyH;
-            __hip_atomic_compare_exchange_strong(&L.tk[s], &cur, h, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (cur == kEmptyH) {  // first occurrence (tc holds occurrences - 1)
-                claimed = true;
-                busy = false;
-            } else if (cur == h) {
-                __hip_atomic_fetch_add(&L.tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                busy = false;
-            } else {
-                s = s + 1 == (uint32_t)kTableSlots ? 0u : s + 1;
-                if (++probes == (uint32_t)kTableSlots) {  // table full
-                    *ovf = 1u;
-                    busy = false;
-                }
-            }
+#ifdef KMC_CANON_PROF
+        ++rounds;
+#endif
+        const unsigned long long cur = lds_cas64(busy ? tk0 + 8u * s : dummy, kEmptyH, h);
+        const bool claimed = busy && cur == kEmptyH;  // first occurrence (tc holds occurrences - 1)
+        const bool dup = busy && cur == h;
+        if (__ballot(dup)) {
+            if (dup) __hip_atomic_fetch_add(&L.tc[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         const uint64_t mc = __ballot(claimed);
-        if (claimed) {
-            const uint32_t at = ncl + (uint32_t)__popcll(mc & lt);
-            if (at < (uint32_t)kClaimW) cl[at] = (uint16_t)s;
-            else *ovf = 1u;
-        }
+        const uint32_t ca = ncl + (uint32_t)__popcll(mc & lt);
+        cl[claimed && ca < cap ? ca : (uint32_t)kClaimW] = (uint16_t)s;
         ncl += (uint32_t)__popcll(mc);
+        busy = busy && !claimed && !dup;
+        s = busy ? ((s + step) & (kTableSlots - 1)) : s;
+        if (ncl > cap) {
+            if (lane == 0) *ovf = 1u;
+            break;
+        }
     }
+#ifdef KMC_CANON_PROF
+    if (lane == 0) {
+        atomicAdd(&g_prof2[0], (unsigned long long)rounds);
+        atomicAdd(&g_prof2[1], (unsigned long long)nq);
+        atomicAdd(&g_prof2[2], 1ull);
+    }
+#endif
+}
+
+// Pass of h among P (a power of two): the top log2 P bits of h's bits [32, 49)
+// (above them: the list bits), so that splitting pass q of P gives passes 2q and
+// 2q + 1 of 2P
+__device__ __forceinline__ uint32_t pass_of(unsigned long long h, uint32_t P) {
+    const int lgP = __builtin_ctz(P);
+    return lgP ? (uint32_t)(h >> (kPassTop - lgP)) & (P - 1u) : 0u;
 }
 
 // The wave's keys of pass q / P, staged in its LDS queue and probed; a queue that
 // fills up (repeats beyond the pass target) is probed and refilled.
 __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes], uint32_t q, uint32_t P, K4Lds &L,
-                                            int wv, uint32_t *ovf, uint32_t &ncl) {
+                                            int wv, uint32_t cap, uint32_t *ovf, uint32_t &ncl) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long *qk = L.qk[wv];
@@ -487,19 +539,33 @@ __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes]
         for (int j = 0; j < kRes; ++j) {
             if (j >= next && nq <= (uint32_t)(kStage - 64)) {
                 const unsigned long long h = kh[j];
-                const bool in = h != kEmptyH && ((uint32_t)(h >> 32) & (P - 1u)) == q;
+                const bool in = h != kEmptyH && pass_of(h, P) == q;
                 const uint64_t m = __ballot(in);
                 if (in) qk[nq + (uint32_t)__popcll(m & lt)] = h;
                 nq += (uint32_t)__popcll(m);
                 next = j + 1;
             }
         }
-        if (nq) probe_staged(L, wv, nq, ovf, ncl);
-    } while (next < kRes);
+        if (nq) probe_staged(L, wv, nq, cap, ovf, ncl);
+    } while (next < kRes && ncl <= cap);
 }
 
-__global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
+#ifdef KMC_CANON_PROF
+// diagnostic build only: per-phase s_memtime cycles of K4, summed over waves
+__device__ unsigned long long g_prof[8];
+#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define PROF_ACC(i, d) pacc[i] += (d)
+#else
+#define PROF_T(v)
+#define PROF_ACC(i, d)
+#endif
+
+__global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_table_kernel(HParams p) {
     __shared__ K4Lds L;
+#ifdef KMC_CANON_PROF
+    unsigned long long pacc[8] = {};
+    PROF_T(tk0);
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -508,6 +574,7 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
         L.tc[i] = 0u;
     }
     if (tid < 2) L.ovf[tid] = 0u;
+    if (tid < 64) L.dummy[tid] = 0ull;
     lds_barrier();
     const int64_t G = gridDim.x;
     int64_t l = blockIdx.x;
@@ -522,6 +589,7 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
     if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
     int par = 0;
     for (; l < p.lists; l += G) {
+        PROF_T(t0);
         uint64_t b2 = 0, e2 = 0;
         if (l + 2 * G < p.lists) {
             b2 = p.list_start[l + 2 * G];
@@ -535,18 +603,25 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
         uint32_t P = 1;
         while ((uint64_t)P * kPassDistinct < n && P < kMaxInitPasses) P <<= 1;
         uint64_t out = b0;  // next free pair of this list's segment
+        PROF_T(t1);
+        PROF_ACC(5, t1 - t0);
         for (uint32_t q = 0; q < P;) {
             uint32_t ncl = 0;
+            PROF_T(ta);
             if (resident) {
-                wave_insert(kr, q, P, L, wv, &L.ovf[par], ncl);
+                wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl);
             } else {
                 for (uint64_t i0 = b0; i0 < e0; i0 += (uint64_t)kResKeys) {
                     load_keys(p.ent, i0, e0, kr);
-                    wave_insert(kr, q, P, L, wv, &L.ovf[par], ncl);
+                    wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl);
                 }
             }
             if (lane == 0) L.ncl[par][wv] = ncl;
+            PROF_T(tb);
+            PROF_ACC(0, tb - ta);
             lds_barrier();
+            PROF_T(tc0);
+            PROF_ACC(1, tc0 - tb);
             const bool ovf = L.ovf[par] != 0u;
             if (tid == 0) L.ovf[par ^ 1] = 0u;  // last read before this barrier
             if (ovf) {
@@ -557,9 +632,13 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
                     L.tc[i] = 0u;
                 }
                 lds_barrier();
+                par ^= 1;
+                if (P == kMaxPasses) {  // > 2^17 x 2 560 distinct keys in one list: out of pass bits
+                    if (tid == 0) *p.err = 1u;
+                    break;
+                }
                 P <<= 1;
                 q <<= 1;
-                par ^= 1;
                 continue;
             }
             uint32_t before = 0, total = 0;
@@ -586,10 +665,16 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
                 }
             }
             out += total;
+            PROF_T(td);
+            PROF_ACC(2, td - tc0);
             lds_barrier();
+            PROF_T(te);
+            PROF_ACC(3, te - td);
+            PROF_ACC(6, 1ull);
             par ^= 1;
             ++q;
         }
+        PROF_T(tf);
         if (tid == 0) p.ndist[l] = (uint32_t)(out - b0);
 #pragma unroll
         for (int j = 0; j < kRes; ++j) kr[j] = kn[j];
@@ -597,7 +682,17 @@ __global__ __launch_bounds__(kCountBlock) void canon_table_kernel(HParams p) {
         e0 = e1;
         b1 = b2;
         e1 = e2;
+#ifdef KMC_CANON_PROF
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetch, charged here
+#endif
+        PROF_T(tg);
+        PROF_ACC(4, tg - tf);
+        PROF_ACC(7, 1ull);
     }
+#ifdef KMC_CANON_PROF
+    if (lane == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_prof[i], pacc[i]);
+#endif
 }
 
 // K5: pairs to their final place; record offsets
@@ -624,6 +719,7 @@ struct HCache {
 };
 std::mutex h_mu;
 std::vector<HCache> h_ws;
+uint32_t h_claim_cap = kClaimW;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -631,6 +727,26 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace kmc
 
 using namespace kmc;
+
+// Test hook (not in kmc.h): K4's per-wave claim capacity, lowered so that the
+// pass-overflow split runs often; 0 restores the default.
+extern "C" int kmc_diag_canon_claim_cap(unsigned cap) {
+    if (cap > (unsigned)kClaimW) return KMC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h_mu);
+    h_claim_cap = cap ? cap : kClaimW;
+    return KMC_OK;
+}
+
+#ifdef KMC_CANON_PROF
+extern "C" int kmc_diag_canon_prof(unsigned long long *host12) {  // read and reset
+    if (hipMemcpyFromSymbol(host12, HIP_SYMBOL(g_prof), 64) != hipSuccess ||
+        hipMemcpyFromSymbol(host12 + 8, HIP_SYMBOL(g_prof2), 32) != hipSuccess)
+        return 1;
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, 64) != hipSuccess ||
+           hipMemcpyToSymbol(HIP_SYMBOL(g_prof2), z, 32) != hipSuccess;
+}
+#endif
 
 extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k,
                                         unsigned flags, uint64_t *keys, uint32_t *counts, uint64_t capacity,
@@ -721,6 +837,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     const size_t o_pc = o; o += al256((size_t)cap_w * 4);
     const size_t o_nd = o; o += al256((size_t)L * 4);
     const size_t o_do = o; o += al256((size_t)(L + 1) * 8);
+    const size_t o_err = o; o += al256(4);
     const size_t total = o;
     char *ws;
     {
@@ -755,6 +872,8 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     p.pc = reinterpret_cast<uint32_t *>(ws + o_pc);
     p.ndist = reinterpret_cast<uint32_t *>(ws + o_nd);
     p.dist_off = reinterpret_cast<uint64_t *>(ws + o_do);
+    p.err = reinterpret_cast<uint32_t *>(ws + o_err);
+    p.claim_cap = h_claim_cap;
     p.rec_off = rec_offsets;
     p.out_keys = keys;
     p.out_counts = counts;
@@ -767,6 +886,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
         (NF && (he = hipMemcpyAsync((void *)p.fsplit, fsplit.data(), NF * sizeof(int2), hipMemcpyHostToDevice,
                                     stream))))
         return (int)he;
+    if ((he = hipMemsetAsync(p.err, 0, 4, stream))) return (int)he;
     if (M > 0) {
         if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream)) ||
             (he = hipMemsetAsync(p.cnt_c, 0, (size_t)Mc * 4, stream)))
@@ -778,16 +898,18 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     hipLaunchKernelGGL(canon_coarse_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
     hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (NF > 0) hipLaunchKernelGGL(canon_fine_kernel, dim3((unsigned)NF), dim3(kWalkBlock), 0, stream, p);
-    // persistent: one workgroup per CU (the table fills its LDS) striding over the lists
-    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, cus))),
+    // persistent: two workgroups per CU (their tables fill the LDS) striding over the lists
+    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 2 * (int64_t)cus))),
                        dim3(kCountBlock), 0, stream, p);
     excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);
     hipLaunchKernelGGL(canon_recoff_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
     uint64_t distinct = 0;
+    uint32_t err = 0;
     if ((he = hipGetLastError()) ||
         (he = hipMemcpyAsync(&distinct, p.dist_off + L, 8, hipMemcpyDeviceToHost, stream)) ||
-        (he = hipStreamSynchronize(stream)))
+        (he = hipMemcpyAsync(&err, p.err, 4, hipMemcpyDeviceToHost, stream)) || (he = hipStreamSynchronize(stream)))
         return (int)he;
+    if (err) return KMC_ERR_INVALID_ARG;  // a record far beyond any genome (see kMaxPasses)
     *num_distinct = distinct;
     if (distinct > capacity) return KMC_ERR_CAPACITY;
     if (distinct && (!keys || !counts)) return KMC_ERR_INVALID_ARG;

@@ -112,6 +112,27 @@ def test_canonical_repetitive_and_many_records(kmc, oracle, cuda):
         assert_same(gpu_canon(kmc, cuda, data, idx, k), oracle.count_canonical(data, idx, k), "k=%d" % k)
 
 
+@pytest.mark.parametrize("cap", [8, 40])
+def test_canonical_pass_overflow_split(kmc, oracle, cuda, cap):
+    """K4's pass split: with the per-wave claim capacity lowered (test hook) most
+    passes overflow and are redone as two passes, recursively; results unchanged.
+    Records from 600 K to 3 M windows (lists of 2-8 K keys), one repetitive."""
+    import ctypes
+    rng = np.random.default_rng(77 + cap)
+    data, idx = random_records(rng, [3_000_000, 600_000, 1_500_001])
+    rep = np.frombuffer(b"ACGTTGCA" * 100_000 + b"A" * 200_000, dtype=np.uint8)
+    data = np.concatenate([data, rep, np.zeros(1, np.uint8)])
+    idx = np.append(idx, data.size)
+    hook = kmc.lib().kmc_diag_canon_claim_cap
+    hook.argtypes = [ctypes.c_uint]
+    assert hook(cap) == 0
+    try:
+        for k in (21, 31):
+            assert_same(gpu_canon(kmc, cuda, data, idx, k), oracle.count_canonical(data, idx, k), "cap=%d k=%d" % (cap, k))
+    finally:
+        assert hook(0) == 0
+
+
 def test_canonical_size_independent_properties(kmc, cuda):
     """64 Mbase: counts sum to the valid windows; canonical == forward folded by revcomp."""
     import torch
