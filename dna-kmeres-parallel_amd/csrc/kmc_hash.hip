@@ -22,12 +22,14 @@
 //               bucket is one list)
 //   K3b fine    one workgroup per coarse bucket of the records with more lists than
 //               buckets: the same staged sort by list, bucket -> its lists
-//   K4 count    workgroups stride over the lists; a list (held in registers, the
-//               next one prefetched) is counted in an LDS open-addressing table
-//               (64-bit CAS claim, 32-bit add for repeats) in as many passes as keep
-//               a pass's distinct keys near 4 K (selected by hash bits 32+); each
-//               pass writes the slots it claimed, in claim order, to the list's
-//               segment and clears only those slots
+//   K4 count    two 512-thread workgroups per CU stride over the lists; a list
+//               (held in registers) is counted in an LDS table (4 096 slots,
+//               double hashing, 64-bit CAS claim, 32-bit add for repeats) in as
+//               many passes as keep a pass near 2 K keys (selected by hash bits
+//               below the list bits); each wave stages its keys of the pass in LDS
+//               and its lanes take them as their probe chains end; the slots each
+//               wave claimed are written (claim order) to the list's segment and
+//               cleared
 //   K5 place    exclusive scan of the distinct counts; each list's pairs are copied
 //               to their final place; records are contiguous runs of lists
 // Bytes per window: the input twice (K1, K3a), an 8-byte h written and read twice
@@ -69,8 +71,11 @@ constexpr int kCountBlock = 512;             // K4 threads per workgroup (two wo
 constexpr int kTableLg = 12;
 constexpr int kTableSlots = 1 << kTableLg;   // K4 LDS table: 4 096 x (8 + 4) B, double hashing
 constexpr int kWaves4 = kCountBlock / 64;
+#ifndef KMC_CANON_KN
+#define KMC_CANON_KN 0  // 1: K4 prefetches the next list's keys into registers (no gain: the CU's other workgroup hides the load)
+#endif
 #ifndef KMC_CANON_STAGE
-#define KMC_CANON_STAGE 256
+#define KMC_CANON_STAGE 320
 #endif
 constexpr int kStage = KMC_CANON_STAGE;                // K4 per-wave keys staged for one probe loop
 constexpr int kClaimW = 320;                 // K4 per-wave claims per pass (2-byte slot ids)
@@ -409,14 +414,17 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
 
 // K4: lists counted in an LDS table, workgroups striding over the lists.  Its
 // barriers are LDS-only (lds_barrier): __syncthreads would also wait for the pair
-// stores and for the next list's key prefetch.
+// stores.
 //
 // An LDS 64-bit CAS costs the LDS ~21 cycles per wave instruction however few
 // lanes are active (scripts/lds_microbench.hip, modes 14/16), so the probe loop
 // keeps every lane busy: each wave stages its keys of the pass in a private LDS
 // queue and its lanes take queue entries as they finish their probe chains.
 // Each wave lists the slots its lanes claimed, so that the write-out and the
-// table clear touch only the pass's distinct keys.
+// table clear touch only the pass's distinct keys.  Measured per pass and wave
+// (scripts/c4_prof.py): ~6 probe rounds for ~150 staged keys; the kernel is
+// bound by the LDS round trips of those rounds and by the barrier waits of the
+// pass structure, not by HBM.
 __device__ __forceinline__ void load_keys(const uint64_t *ent, uint64_t i0, uint64_t end,
                                           unsigned long long (&kh)[kRes]) {
 #pragma unroll
@@ -585,8 +593,11 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         b1 = p.list_start[l + G];
         e1 = p.list_start[l + G + 1];
     }
-    unsigned long long kr[kRes], kn[kRes];
+    unsigned long long kr[kRes];
+#if KMC_CANON_KN
+    unsigned long long kn[kRes];
     if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
+#endif
     int par = 0;
     for (; l < p.lists; l += G) {
         PROF_T(t0);
@@ -595,7 +606,11 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
             b2 = p.list_start[l + 2 * G];
             e2 = p.list_start[l + 2 * G + 1];
         }
+#if KMC_CANON_KN
         if (l + G < p.lists && e1 - b1 <= (uint64_t)kResKeys) load_keys(p.ent, b1, e1, kn);
+#else
+        if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
+#endif
         const uint64_t n = e0 - b0;
         const bool resident = n <= (uint64_t)kResKeys;
         // passes from the list length, capped: repeats do not need passes, and a
@@ -676,8 +691,10 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         }
         PROF_T(tf);
         if (tid == 0) p.ndist[l] = (uint32_t)(out - b0);
+#if KMC_CANON_KN
 #pragma unroll
         for (int j = 0; j < kRes; ++j) kr[j] = kn[j];
+#endif
         b0 = b1;
         e0 = e1;
         b1 = b2;

@@ -1,7 +1,7 @@
 # GPU: configs C3 (k=13 radix) and C4 (k=31 canonical) under a rocprofv3 kernel trace;
 # prints the JSON lines and the per-kernel summary.
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out/cb && rm -rf gpurun_out/cb/*
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cb -o cb -- python3 scripts/cbench.py --iters ${ITERS:-2} ${CB_ARGS} > gpurun_out/cb/log 2>&1 || { tail -20 gpurun_out/cb/log; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cb -o cb -- python3 scripts/cbench.py --iters ${ITERS:-3} ${CB_ARGS} > gpurun_out/cb/log 2>&1 || { tail -20 gpurun_out/cb/log; exit 1; }
 grep '^{' gpurun_out/cb/log
 python3 - <<'PY'
 import csv, glob
