@@ -525,12 +525,11 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
 #endif
 }
 
-// Pass of h among P (a power of two): the top log2 P bits of h's bits [32, 49)
-// (above them: the list bits), so that splitting pass q of P gives passes 2q and
-// 2q + 1 of 2P
+// Pass of h among P: the P-quantile of h's bits [32, kPassTop) (above them: the
+// list bits), so that splitting pass q of P gives passes 2q and 2q + 1 of 2P
 __device__ __forceinline__ uint32_t pass_of(unsigned long long h, uint32_t P) {
-    const int lgP = __builtin_ctz(P);
-    return lgP ? (uint32_t)(h >> (kPassTop - lgP)) & (P - 1u) : 0u;
+    constexpr int kBits = kPassTop - 32;
+    return (uint32_t)((((h >> 32) & ((1ull << kBits) - 1ull)) * (uint64_t)P) >> kBits);
 }
 
 // The wave's keys of pass q / P, staged in its LDS queue and probed; a queue that
@@ -616,7 +615,8 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         // passes from the list length, capped: repeats do not need passes, and a
         // pass with too many distinct keys overflows and splits
         uint32_t P = 1;
-        while ((uint64_t)P * kPassDistinct < n && P < kMaxInitPasses) P <<= 1;
+        if (n > (uint64_t)kPassDistinct)
+            P = (uint32_t)std::min<uint64_t>(kMaxInitPasses, (n + kPassDistinct - 1) / kPassDistinct);
         uint64_t out = b0;  // next free pair of this list's segment
         PROF_T(t1);
         PROF_ACC(5, t1 - t0);
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 }
                 lds_barrier();
                 par ^= 1;
-                if (P == kMaxPasses) {  // > 2^17 x 2 560 distinct keys in one list: out of pass bits
+                if (P >= kMaxPasses) {  // > 2^17 x 2 560 distinct keys in one list: out of pass bits
                     if (tid == 0) *p.err = 1u;
                     break;
                 }
