@@ -43,10 +43,18 @@
 namespace kmc {
 namespace {
 
-// Low code bits resolved by the per-list LDS histogram (2^low x 32-bit, at most
+// Low code bits resolved by the per-list LDS histogram (2^low bins, at most
 // 128 KB); the rest select the bucket.  At least 64 buckets per record, so the
 // bucket counters of R1/R3 see few same-address LDS atomics.
-__host__ __device__ constexpr int low_bits(int k) { return 2 * k - 6 < 15 ? 2 * k - 6 : 15; }
+#ifndef KMC_RADIX_LOW_MAX
+#define KMC_RADIX_LOW_MAX 16
+#endif
+// (16 low bits — two 16-bit R4 bins per LDS word — from k = 12 on: half the
+// buckets, so R3's runs per bucket and round are twice as long; at k = 11 the
+// 64 buckets per record would leave R4 too few workgroups)
+__host__ __device__ constexpr int low_bits(int k) {
+    return 2 * k - 6 < (k >= 12 ? KMC_RADIX_LOW_MAX : 15) ? 2 * k - 6 : (k >= 12 ? KMC_RADIX_LOW_MAX : 15);
+}
 
 struct RParams {
     const char *data;
@@ -270,38 +278,90 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
 
 // R4: one workgroup per list (s, b).
 template <int LOW>
-__global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbins) {
-    constexpr int kBucketBins = 1 << LOW;
-    __shared__ __attribute__((aligned(16))) uint32_t h[kBucketBins];
-    const int64_t list = blockIdx.x;  // s*nbk + b
-    const int64_t s = list / p.nbk, b = list % p.nbk;
-    for (int i = threadIdx.x; i < kBucketBins; i += 1024) h[i] = 0u;
-    __syncthreads();
-    const uint64_t beg = p.off[list * p.G], end = p.off[(list + 1) * p.G];
+__device__ __forceinline__ void hist_add(uint32_t *h, uint32_t e) {
+    if constexpr (LOW <= 15) {
+        __hip_atomic_fetch_add(&h[e], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {  // two 16-bit bins per word
+        __hip_atomic_fetch_add(&h[e >> 1], (e & 1u) ? 0x10000u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// The entries [beg, end) of one list into h (hist_add<LOW>); entries whose top
+// bit differs from `half` are skipped when HALF (the 32-bit recount of LOW = 16).
+template <int LOW, bool HALF>
+__device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uint64_t end, uint32_t *h, uint32_t half) {
+    const auto add = [&](uint32_t e) {
+        if constexpr (HALF) {
+            if ((e >> 15) == half) __hip_atomic_fetch_add(&h[e & 0x7FFFu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            hist_add<LOW>(h, e);
+        }
+    };
     // head up to 8-entry alignment, 16-B vector body, tail
     uint64_t a = beg;
     const uint64_t abody = (beg + 7) & ~(uint64_t)7;
-    if (a + threadIdx.x < (abody < end ? abody : end))
-        atomicAdd(&h[p.ent[a + threadIdx.x]], 1u);
+    if (a + threadIdx.x < (abody < end ? abody : end)) add(ent[a + threadIdx.x]);
     a = abody;
     if (a < end) {
         const uint64_t nvec = (end - a) / 8;
-        const uint4 *v = reinterpret_cast<const uint4 *>(p.ent + a);
+        const uint4 *v = reinterpret_cast<const uint4 *>(ent + a);
         for (uint64_t i = threadIdx.x; i < nvec; i += 1024) {
             const uint4 x = v[i];
             const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                __hip_atomic_fetch_add(&h[w[q] & 0xFFFFu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&h[w[q] >> 16], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                add(w[q] & 0xFFFFu);
+                add(w[q] >> 16);
             }
         }
         const uint64_t t = a + nvec * 8;
-        if (t + threadIdx.x < end) atomicAdd(&h[p.ent[t + threadIdx.x]], 1u);
+        if (t + threadIdx.x < end) add(ent[t + threadIdx.x]);
     }
+}
+
+// R4: one workgroup per list (s, b): 2^LOW-bin LDS histogram -> stage.  LOW = 16
+// packs two 16-bit bins per word (128 KB); a bin that reaches 65 536 within the
+// list wraps, which lowers the sum of the bins below the list length (a carry
+// into the neighbour costs 65 535, one out of the word 65 536), and the list is
+// then recounted exactly in two 32 768-bin halves.
+template <int LOW>
+__global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbins) {
+    constexpr int kBucketBins = 1 << LOW;
+    constexpr int kWords = LOW <= 15 ? kBucketBins : kBucketBins / 2;
+    __shared__ __attribute__((aligned(16))) uint32_t h[kWords];
+    __shared__ unsigned long long s_sum;
+    const int64_t list = blockIdx.x;  // s*nbk + b
+    const int64_t s = list / p.nbk, b = list % p.nbk;
+    for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+    if (threadIdx.x == 0) s_sum = 0ull;
+    __syncthreads();
+    const uint64_t beg = p.off[list * p.G], end = p.off[(list + 1) * p.G];
+    hist_list<LOW, false>(p.ent, beg, end, h, 0u);
     __syncthreads();
     uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
-    for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
+    if constexpr (LOW <= 15) {
+        for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
+    } else {
+        uint32_t part = 0u;
+        for (int i = threadIdx.x; i < kWords; i += 1024) part += (h[i] & 0xFFFFu) + (h[i] >> 16);
+        atomicAdd(&s_sum, (unsigned long long)part);
+        __syncthreads();
+        if (s_sum == end - beg) {
+            for (int i = threadIdx.x; i < kWords; i += 1024) {
+                const uint32_t w = h[i];
+                reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
+            }
+        } else {  // a bin wrapped: exact recount, half of the bins at a time
+            for (uint32_t half = 0; half < 2; ++half) {
+                __syncthreads();
+                for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+                __syncthreads();
+                hist_list<LOW, true>(p.ent, beg, end, h, half);
+                __syncthreads();
+                for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
+            }
+        }
+    }
 }
 
 // R5: stage [n][nbins] -> sum[s + ld*code]; one workgroup per 256 codes.

@@ -125,6 +125,28 @@ def test_radix_k9_13_vs_oracle(kmc, oracle, cuda, k):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
+@pytest.mark.parametrize("k", [11, 12, 13])
+def test_radix_wrapping_bins_recounted(kmc, oracle, cuda, k):
+    """k >= 12 keeps two 16-bit bins per LDS word in R4: a k-mer seen >= 65 536
+    times in one list (poly-A / poly-AC runs) wraps its bin and the list is
+    recounted exactly; lists without a wrap keep the packed result (k = 11: the
+    32-bit bins, same input)."""
+    rng = np.random.default_rng(4100 + k)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    poly = np.full(300_000, ord("A"), np.uint8)
+    di = np.frombuffer(b"AC" * 70_000, np.uint8)
+    mixed = np.concatenate([acgt[rng.integers(0, 4, 500_000)], poly, acgt[rng.integers(0, 4, 200_000)], di])
+    recs = [np.append(mixed, np.uint8(0)), np.append(acgt[rng.integers(0, 4, 1_000_000)], np.uint8(0)),
+            np.append(poly[:70_000], np.uint8(0))]
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    assert exp[0, 0] > 65_536  # AAAA...A in record 0
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
 @pytest.mark.parametrize("k", [11, 13])
 def test_radix_shards_sum_to_full(kmc, oracle, cuda, k):
     import torch
