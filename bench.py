@@ -115,8 +115,9 @@ def main():
     stream = torch.cuda.current_stream()
 
     def step():
-        counts.zero_()
-        kmc.count_dense_ex(a, stream)
+        if world > 1:  # the other ranks' columns: zero before the summing all-reduce
+            counts.zero_()
+        kmc.count_dense_ex(a, stream)  # overwrites every entry of this rank's columns
         if world > 1:
             dist.all_reduce(counts)
 
