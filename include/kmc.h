@@ -190,8 +190,8 @@ int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq, int *i
  * rec_offsets and KMC_ERR_CAPACITY is returned (valid windows, <= data bytes,
  * always suffice).  data 16-byte aligned with data[p] = byte p of the global
  * offsets in `indices` (device int64[num_seqs + 1]).  Synchronous on `stream`
- * (the distinct total is returned to the host); table memory is library-owned,
- * about 17 bytes per window. */
+ * (the distinct total is returned to the host); workspace memory is
+ * library-owned, about 20 bytes per window (no hash table lives in HBM). */
 #define KMC_CANON_MAX_K 31
 #define KMC_CANON_SOFTMASK 1u
 #define KMC_CANON_FORWARD 2u
