@@ -4,11 +4,12 @@
 Workload (BASELINE.json configs[1]): 10 Gbase per GPU as 10 records of 1 Gbase,
 k = 8 (65 536-bin dense histogram), the synthetic layout of SURVEY.md §8(d)
 (uniform iid ACGT from splitmix64, seed 0x5EED0000 + k, one '\\0' after each
-record).  One step = one full pass of the hot path over the batch:
-zero the count matrix, count every window of every record
-(kmc_count_dense_ex: histogram kernel + slab reduce + spill fix-up), and, for
-N > 1, the RCCL all-reduce of the int32 count matrix (records sharded by rank:
-weak scaling, 10 Gbase per GPU; the N-rank job is one 10N-Gbase FASTA).
+record).  One step = one full pass of the hot path over the batch: count every
+window of every record (kmc_count_dense_ex: histogram kernel + slab reduce +
+spill fix-up; it overwrites every entry of the rank's columns), and, for N > 1,
+zero the other ranks' columns and the RCCL all-reduce of the int32 count matrix
+(records sharded by rank: weak scaling, 10 Gbase per GPU; the N-rank job is one
+10N-Gbase FASTA).
 
 Printed (rank 0, one JSON line): metric/value/unit as BASELINE.json, roofline of
 the histogram kernel (algorithmic bytes = input ASCII bytes + int32 output,
