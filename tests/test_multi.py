@@ -95,3 +95,57 @@ def test_gloo_world2_shard_allreduce(k):
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
     assert res[0][2] == res[1][2]
+
+
+def _overlap_worker(rank, world, port, steps, q):
+    """bench.py's overlapped steps with a CPU stand-in for the count: each step
+    writes rank- and step-specific values into this rank's columns; after the
+    async gloo all-reduces every matrix must hold the sum over ranks of its last
+    step's columns."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nb, n_loc = 64, 3
+    n_tot = n_loc * world
+    bufs = [torch.full((nb, n_tot), -7, dtype=torch.int32) for _ in range(2)]
+    last_step = [None, None]
+
+    def count(j):  # this rank's columns only, every entry overwritten
+        i = last_step[j]
+        cols = torch.arange(n_loc, dtype=torch.int32) + rank * n_loc
+        bufs[j][:, rank * n_loc:(rank + 1) * n_loc] = (i * 1000 + cols)[None, :] + torch.arange(nb, dtype=torch.int32)[:, None]
+
+    step, drain = bench.overlapped_steps(bufs, count, world, dist.all_reduce)
+    ok = True
+    for i in range(steps):
+        j = i % 2
+        last_step[j] = i
+        step(i)
+    drain()
+    for j in range(2):
+        i = last_step[j]
+        exp = (i * 1000 + torch.arange(n_tot, dtype=torch.int32))[None, :] + torch.arange(nb, dtype=torch.int32)[:, None]
+        ok = ok and bool(torch.equal(bufs[j], exp))
+    q.put((rank, ok))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_overlapped_allreduce():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, 7, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok in res), res
