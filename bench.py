@@ -36,7 +36,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=14)  # the clocks settle over ~10 launches
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--records", type=int, default=10, help="records per GPU")
     ap.add_argument("--record-len", type=int, default=1_000_000_000, help="bases per record")
@@ -153,22 +153,28 @@ def main():
 
     step, drain = overlapped_steps(bufs, count, world, dist.all_reduce if world > 1 else None)
 
-    last = 0
-    for i in range(args.warmup):
-        last = step(i)
-    drain()
-    torch.cuda.synchronize()
-    # correctness guard on the warm result (cheap, outside the timed region):
-    # every window of the synthetic input is valid, so each record's column sums to L-k+1
-    tot = bufs[last].to(torch.int64).sum(dim=0)
-    if not bool((tot == (L - k + 1)).all()):
-        raise SystemExit("count check failed: column sums %s" % tot[:4].tolist())
-
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for b, e in ev:  # materialise the events before handing them to the library
         b.record(stream)
         e.record(stream)
+    # warm-up: the correctness guard runs on an early warm result, and the last
+    # warm-up steps follow it, so that the clocks that dropped while the host
+    # checked are back up when the timed steps start (after idling, the GPU ramps
+    # its clock over ~10 launches of this kernel: profiles/r01_kernel_launches.json)
+    n_after = min(12, max(args.warmup - 1, 0))
+    last = 0
+    for i in range(args.warmup - n_after):
+        last = step(i)
+    drain()
     torch.cuda.synchronize()
+    if args.warmup > 0:
+        # every window of the synthetic input is valid, so each record's column sums to L-k+1
+        tot = bufs[last].to(torch.int64).sum(dim=0)
+        if not bool((tot == (L - k + 1)).all()):
+            raise SystemExit("count check failed: column sums %s" % tot[:4].tolist())
+    for i in range(args.warmup - n_after, args.warmup):
+        step(i)
+    drain()
 
     if world > 1:
         dist.barrier()

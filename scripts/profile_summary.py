@@ -2,6 +2,7 @@
 """Turn gpurun_out/prof_bench/ (scripts/profile_bench.sh) into committed profiles/:
   profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary of the bench command
   profiles/<tag>_bench_trace.json   the bench JSON line printed under the profiler
+  profiles/<tag>_kernel_launches.json  per-launch durations of the histogram kernel
   profiles/pmc_dense_k8_10gbase.json  HBM bytes per histogram launch (bench.py reads it)
 FETCH_SIZE is counted in KiB and, on gfx950, reads half the bytes of a wide
 streaming read (MI355X_MICROARCH.md §HBM): bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024."""
@@ -43,6 +44,16 @@ def main():
             json.dump(line, fh, indent=1)
     k = line["config"]["k"] if line else 8
     kern = "count_dense_kernel<%d, 1, 3," % k if k == 8 else "count_dense_kernel<%d," % k
+    # per-launch durations of the histogram kernel, in launch order (warm-up first)
+    traces = glob.glob(os.path.join(SRC, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    if traces:
+        with open(traces[0]) as fh:
+            rows = [r for r in csv.DictReader(fh) if kern in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        ms = [round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6, 4) for r in rows]
+        with open(os.path.join(DST, "%s_kernel_launches.json" % tag), "w") as fh:
+            json.dump({"kernel": kern + " (histogram launches of the bench command, in order)",
+                       "ms": ms}, fh)
     fetch = per_launch(os.path.join(SRC, "fetch"), "FETCH_SIZE", kern)
     write = per_launch(os.path.join(SRC, "write"), "WRITE_SIZE", kern)
     r128 = per_launch(os.path.join(SRC, "fetch"), "TCC_EA0_RDREQ_128B", kern)
