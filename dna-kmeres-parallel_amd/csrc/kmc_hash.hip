@@ -107,7 +107,7 @@ struct HParams {
     uint32_t *cnt_c;         // [Mc] windows per (record, coarse bucket, workgroup)
     uint64_t *off_c;         // [Mc + 1] exclusive scan of cnt_c
     uint64_t *ent;           // [windows] h, list by list
-    uint64_t *ent_c;         // [windows] h, coarse bucket by bucket (K3a -> K3b; aliases pk)
+    uint64_t *ent_c;         // [windows] partition values, coarse bucket by bucket (K3a -> K3b; aliases pk)
     uint64_t *list_start;    // [lists + 1]
     const int2 *fsplit;      // [K3b workgroups] (record, coarse bucket)
     uint64_t *pk;            // [windows] K4 pairs: keys
@@ -131,6 +131,17 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t h) {  // MurmurHash3 finalis
     return h;
 }
 
+// Partition value of a key: K1 / K3a / K3b bucket and list by its top bits.  A
+// multiplicative hash (one 64-bit multiply, invertible) instead of fmix64 in
+// the two input walks; K3b (or K3a for single-list buckets) turns it into
+// fmix64(key) when writing the lists, which is what K4 hashes and unmixes.
+#ifndef KMC_CANON_MULPART
+#define KMC_CANON_MULPART 1
+#endif
+constexpr uint64_t kMulC = 0x9E3779B97F4A7C15ull, kMulCinv = 0xF1DE83E19937733Dull;
+__device__ __forceinline__ uint64_t part_of(uint64_t key);
+__device__ __forceinline__ uint64_t list_value(uint64_t m);
+
 __device__ __forceinline__ uint64_t unmix64(uint64_t h) {  // inverse of fmix64
     h ^= h >> 33;
     h *= 0x9CB4B2F8129337DBull;
@@ -138,6 +149,22 @@ __device__ __forceinline__ uint64_t unmix64(uint64_t h) {  // inverse of fmix64
     h *= 0x4F74430C22A54005ull;
     h ^= h >> 33;
     return h;
+}
+
+__device__ __forceinline__ uint64_t part_of(uint64_t key) {
+#if KMC_CANON_MULPART
+    return key * kMulC;
+#else
+    return fmix64(key);
+#endif
+}
+
+__device__ __forceinline__ uint64_t list_value(uint64_t m) {  // partition value -> fmix64(key)
+#if KMC_CANON_MULPART
+    return fmix64(m * kMulCinv);
+#else
+    return m;
+#endif
 }
 
 // LE 2-bit code (first base in the low bits, the dense path's order) -> MSB-first
@@ -189,7 +216,7 @@ __device__ __forceinline__ uint32_t chunk_keys(const HParams &p, int64_t q, int6
         const bool v = pos >= ps && pos < last && !((badm >> j) & wmask);
         const uint64_t le = (j == 0 ? lo64 : ((lo64 >> (2 * j)) | ((uint64_t)cd[2] << (64 - 2 * j)))) & kmask;
         const uint64_t fw = reverse_groups(le, k);
-        h[j] = fmix64(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
+        h[j] = part_of(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
         vm |= v ? 1u << j : 0u;
     }
     return vm;
@@ -271,9 +298,9 @@ struct Stage {
     unsigned long long *del;
 };
 
-template <class Bk>
+template <class Bk, class Out>
 __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, const unsigned long long (&h)[16],
-                                             uint32_t vm, Bk bk, uint64_t *dst) {
+                                             uint32_t vm, Bk bk, Out out, uint64_t *dst) {
     const int tid = threadIdx.x, lane = tid & 63;
     uint32_t *cn = s.cnt[par];
     uint32_t rk[8];
@@ -325,7 +352,7 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
     lds_barrier();
     for (uint32_t i = tid; i < total; i += kWalkBlock) {
         const unsigned long long x = s.stage[i];
-        dst[s.del[bk(x)] + i] = x;
+        dst[s.del[bk(x)] + i] = out(x);
     }
     // the next round writes stage / del only after two barriers, which every
     // thread reaches after this write-out
@@ -357,7 +384,10 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
             unsigned long long h[16];
             uint32_t vm = 0u;
             if (c < c1) vm = chunk_keys(p, c << 4, ps, pe, rend, h);
-            staged_round(st, par, nbk, h, vm, bk, dst);
+            if (lg > lgc)
+                staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return x; }, dst);
+            else  // buckets are the lists
+                staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return list_value(x); }, dst);
             par ^= 1;
         }
         __syncthreads();
@@ -407,7 +437,7 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
             h[j] = i < a1 ? p.ent_c[i] : 0ull;
             vm |= i < a1 ? 1u << j : 0u;
         }
-        staged_round(st, par, F, h, vm, bk, p.ent);
+        staged_round(st, par, F, h, vm, bk, [](unsigned long long x) { return list_value(x); }, p.ent);
         par ^= 1;
     }
 }
