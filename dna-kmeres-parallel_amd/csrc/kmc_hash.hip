@@ -7,10 +7,11 @@
 // min(key(window), key(reverse complement)) unless KMC_CANON_FORWARD is given.
 //
 // Hash-partitioned counting, so that no table lives in HBM and no k-mer costs a
-// device-scope atomic.  A window travels as h = fmix64(key) (a bijection; only the
-// distinct keys are unmixed, at output).  Record r has 2^lg_r lists (top lg_r bits
-// of h, about 4 K windows each, lg_r <= 14), grouped in 2^lgc_r coarse buckets
-// (top lgc_r = min(lg_r, 7) bits):
+// device-scope atomic.  The input walks partition a window by m = key x C (one
+// multiply, invertible); the lists hold h = fmix64(key) (a bijection; only the
+// distinct keys are unmixed, at output).  Record r has 2^lg_r lists (top lg_r
+// bits of m, about 4 K windows each, lg_r <= 15), grouped in 2^lgc_r coarse
+// buckets (top lgc_r = min(lg_r, 7) bits):
 //   K1 count    workgroups walk contiguous chunk ranges record piece by record
 //               piece; per-piece LDS counters -> windows per (r, list, workgroup)
 //               and per (r, coarse bucket, workgroup)
