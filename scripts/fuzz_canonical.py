@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""DIAGNOSTIC fuzz: kmc_count_canonical_hash vs the oracle on random record sets
+(sizes from 0 to a few M bases, N runs, lowercase, low-complexity runs), random k,
+flags and K4 claim capacities (the test hook), bit-exact per record.
+Usage: python scripts/fuzz_canonical.py [--cases 40] [--seed 1]"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "dna-kmeres-parallel_amd"), os.path.join(REPO, "oracle")]
+
+
+def make_case(rng):
+    n = int(rng.choice([1, 2, 3, 7, 40, 300]))
+    recs = []
+    for _ in range(n):
+        L = int(rng.choice([0, 1, 30, 31, 32, 1000, 40_000, 300_000, 1_500_000]))
+        if n > 40:
+            L = min(L, 20_000)
+        x = rng.choice(np.frombuffer(b"ACGTacgtN", np.uint8), size=L,
+                       p=[.23, .23, .23, .23, .02, .02, .02, .01, .01]).astype(np.uint8)
+        if L > 1000 and rng.random() < 0.4:  # a low-complexity run
+            a = int(rng.integers(0, L - 500))
+            b = min(L, a + int(rng.integers(500, 200_000)))
+            unit = rng.choice([b"A", b"AC", b"ACGTTGCA", b"AAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAT"])
+            x[a:b] = np.resize(np.frombuffer(unit, np.uint8), b - a)
+        recs.append(np.append(x, np.uint8(0)))
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    return data, idx
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=40)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args()
+    import torch
+    import kmc
+    import oracle
+    dev = torch.device("cuda:0")
+    hook = kmc.lib().kmc_diag_canon_claim_cap
+    hook.argtypes = [ctypes.c_uint]
+    rng = np.random.default_rng(a.seed)
+    bad = 0
+    for c in range(a.cases):
+        data, idx = make_case(rng)
+        k = int(rng.choice([1, 5, 11, 17, 21, 27, 31]))
+        flags = int(rng.choice([0, 1, 2, 3]))
+        cap = int(rng.choice([0, 0, 0, 8, 64, 200]))
+        assert hook(cap) == 0
+        d = torch.from_numpy(data if data.size else np.zeros(16, np.uint8)).to(dev)
+        keys, counts, off = kmc.count_canonical(d, torch.from_numpy(idx).to(dev), k, flags=flags,
+                                                capacity=max(data.size, 1))
+        torch.cuda.synchronize()
+        gk, gc, go = keys.cpu().numpy().view(np.uint64), counts.cpu().numpy().view(np.uint32), off.cpu().numpy()
+        ek, ec, eo = oracle.count_canonical(data, idx, k, soft=bool(flags & 1), forward=bool(flags & 2))
+        ok = np.array_equal(go, eo)
+        for s in range(idx.size - 1):
+            if not ok:
+                break
+            ga, gb, ea, eb = int(go[s]), int(go[s + 1]), int(eo[s]), int(eo[s + 1])
+            o1, o2 = np.argsort(gk[ga:gb]), np.argsort(ek[ea:eb])
+            ok = np.array_equal(gk[ga:gb][o1], ek[ea:eb][o2]) and np.array_equal(gc[ga:gb][o1], ec[ea:eb][o2])
+        print("case %2d: %4d records %9d bytes k=%2d flags=%d cap=%3d %s" % (c, idx.size - 1, data.size, k, flags,
+                                                                         cap, "ok" if ok else "MISMATCH"), flush=True)
+        bad += not ok
+    hook(0)
+    print("fuzz: %d/%d cases bit-exact" % (a.cases - bad, a.cases))
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
