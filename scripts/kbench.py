@@ -32,7 +32,7 @@ def main():
         args = kmc.dense_args(data, idx, k, out)
         ws = torch.empty(kmc.dense_ex_workspace_size(args), dtype=torch.uint8, device=dev)
         args = kmc.dense_args(data, idx, k, out, workspace=ws)
-        for _ in range(2):
+        for _ in range(10):  # the clock ramps over ~10 launches after idling
             kmc.count_dense_ex(args)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
         for b, e in ev:
