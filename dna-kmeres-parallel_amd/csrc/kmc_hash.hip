@@ -68,8 +68,14 @@ constexpr int kCoarseLg = 7;                 // at most 128 coarse buckets per r
 constexpr int kMaxBk = 1 << (kMaxLg - kCoarseLg);  // buckets of one staged round (coarse, or lists per bucket)
 constexpr int64_t kListTarget = 4096;        // windows per list aimed at
 constexpr int kRound = 16 * kWalkBlock;      // K3a / K3b windows per staged round
-constexpr int kCountBlock = 512;             // K4 threads per workgroup (two workgroups per CU)
-constexpr int kTableLg = 12;
+#ifndef KMC_CANON_BLOCK
+#define KMC_CANON_BLOCK 512
+#endif
+#ifndef KMC_CANON_TLG
+#define KMC_CANON_TLG 12
+#endif
+constexpr int kCountBlock = KMC_CANON_BLOCK;  // K4 threads per workgroup (1024 / kCountBlock workgroups per CU)
+constexpr int kTableLg = KMC_CANON_TLG;
 constexpr int kTableSlots = 1 << kTableLg;   // K4 LDS table: 4 096 x (8 + 4) B, double hashing
 constexpr int kWaves4 = kCountBlock / 64;
 #ifndef KMC_CANON_KN
@@ -947,7 +953,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (NF > 0) hipLaunchKernelGGL(canon_fine_kernel, dim3((unsigned)NF), dim3(kWalkBlock), 0, stream, p);
     // persistent: two workgroups per CU (their tables fill the LDS) striding over the lists
-    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 2 * (int64_t)cus))),
+    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (1024 / kCountBlock) * (int64_t)cus))),
                        dim3(kCountBlock), 0, stream, p);
     excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);
     hipLaunchKernelGGL(canon_recoff_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
