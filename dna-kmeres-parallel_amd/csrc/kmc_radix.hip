@@ -39,6 +39,15 @@
 #ifndef KMC_RSCAT_PF
 #define KMC_RSCAT_PF 2
 #endif
+// tiles per wave in one R3 round (the round is counting-sorted in LDS: 64 KB of
+// staging per tile and wave group)
+#ifndef KMC_RSCAT_RT
+#define KMC_RSCAT_RT 2
+#endif
+// write-out loop unroll (entries in flight per lane; register pressure)
+#ifndef KMC_RSCAT_WU
+#define KMC_RSCAT_WU 16
+#endif
 
 namespace kmc {
 namespace {
@@ -92,21 +101,23 @@ struct RCountOp {
 };
 
 // R3 op.  Scattering every window straight to its list costs one L2 write
-// request per 2-byte entry (64 per wave store); instead each round of one tile
+// request per 2-byte entry (64 per wave store); instead each round of RT tiles
 // per wave is counting-sorted by bucket in LDS and written out so that
 // consecutive lanes store consecutive entries of one list.  A window's rank in
-// its bucket is taken (returning LDS add) as the tile is decoded, and the window
-// stays in registers (code + rank) until the round's scan has placed the buckets.
-//   srt  [NW*1024]   the round sorted by bucket
-//   off  [NBK + 1]   bucket counts -> exclusive offsets within srt
-//   gcur [NBK]       global position of each list's next entry (this workgroup)
-//   gdel [NBK]       this round: global position of srt index 0 of each bucket's run
+// its bucket is taken (returning LDS add) as the tile is decoded; the lane keeps
+// only the tile's bases (lo, hi, valid mask) and the ranks, and recomputes the
+// codes once the round's scan has placed the buckets.
+//   srt  [NW*1024*RT] the round sorted by bucket
+//   off  [NBK + 1]    bucket counts -> exclusive offsets within srt
+//   gcur [NBK]        global position of each list's next entry (this workgroup)
+//   gdel [NBK]        this round: global position of srt index 0 of each bucket's run
 // Only buckets [b_lo, b_lo + b_n) are scattered (bucket-group launches).
-template <int K, int NW>
+template <int K, int NW, int RT>
 struct RStageOp {
     static constexpr int LOW = low_bits(K);
     static constexpr int NBK = 1 << (2 * K - LOW);
-    static constexpr int BATCH = NW * 1024;
+    static constexpr int BATCH = NW * 1024 * RT;
+    static_assert(BATCH <= 65536, "ranks are 16-bit");
     static constexpr uint32_t kNone = 0xFFFFFFFFu;
     uint32_t *srt, *off, *nw;
     unsigned long long *gcur;
@@ -114,29 +125,52 @@ struct RStageOp {
     uint16_t *ent;
     uint32_t b_lo, b_n;
     int wave, lane, tid;
-    uint32_t code[16];  // this round's windows of the lane (kNone: none)
-    uint32_t rank[8];   // their ranks in their buckets, two 16-bit ranks per word (< BATCH)
+    int slot;              // tiles of this round held (workgroup-uniform)
+    uint32_t lo[RT], hi[RT], wm[RT];  // per held tile: bases and windows taken (0: none)
+    uint32_t rank[RT][8];  // their ranks in their buckets, two 16-bit ranks per word (< BATCH)
 
     __device__ void before_tile() {}
 
-    template <bool MASKED>
-    __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
+    __device__ __forceinline__ bool take(uint32_t c, uint32_t W, int j) const {
+        return ((W >> j) & 1u) && ((c >> LOW) - b_lo) < b_n;
+    }
+
+    template <int S>
+    __device__ __forceinline__ void rank_tile(uint32_t l, uint32_t h, uint32_t W) {
+        lo[S] = l;
+        hi[S] = h;
+        uint32_t m = 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const uint32_t c = window_code_rt<K>(lo, hi, j);
-            const bool v = (!MASKED || ((W >> j) & 1u)) && ((c >> LOW) - b_lo) < b_n;
+            const uint32_t c = window_code_rt<K>(l, h, j);
+            const bool v = take(c, W, j);
             uint32_t r = 0;
             if (v) r = __hip_atomic_fetch_add(&off[(c >> LOW) - b_lo], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            code[j] = v ? c : kNone;
-            if (j & 1) rank[j >> 1] |= r << 16;
-            else rank[j >> 1] = r;
+            m |= (uint32_t)v << j;
+            if (j & 1) rank[S][j >> 1] |= r << 16;
+            else rank[S][j >> 1] = r;
+        }
+        wm[S] = m;
+    }
+
+    template <bool MASKED>
+    __device__ __forceinline__ void tile(uint32_t l, uint32_t h, uint32_t W) {
+        if constexpr (RT == 1) {
+            rank_tile<0>(l, h, W);
+        } else {
+            static_assert(RT == 2, "one or two tiles per round");
+            if (slot == 0) rank_tile<0>(l, h, W);
+            else rank_tile<1>(l, h, W);
         }
     }
 
-    __device__ void after_iter(int64_t, int64_t, bool) {
+    __device__ void after_iter(int64_t i, int64_t per, bool) {
+        if (++slot < RT && i + 1 < per) return;  // round not full (i, per, slot: workgroup-uniform)
+        slot = 0;
         lds_barrier();  // every rank taken
 #if KMC_RSCAT_ABL == 3
-        for (int j = 0; j < 16; ++j) code[j] = kNone;
+#pragma unroll
+        for (int S = 0; S < RT; ++S) wm[S] = 0u;
         lds_barrier();
         return;  // diagnostic: ranking only
 #endif
@@ -145,9 +179,15 @@ struct RStageOp {
         // counting-sort the round into srt; per bucket, the global position of srt
         // index 0 (gdel = cursor - offset) and the advanced cursor
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (code[j] != kNone)
-                srt[off[(code[j] >> LOW) - b_lo] + ((rank[j >> 1] >> (16 * (j & 1))) & 0xFFFFu)] = code[j];
+        for (int S = 0; S < RT; ++S) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t c = window_code_rt<K>(lo[S], hi[S], j);
+                if ((wm[S] >> j) & 1u)
+                    srt[off[(c >> LOW) - b_lo] + ((rank[S][j >> 1] >> (16 * (j & 1))) & 0xFFFFu)] = c;
+            }
+            wm[S] = 0u;
+        }
         for (uint32_t b = tid; b < b_n; b += NW * 64) {
             const uint32_t o0 = off[b], o1 = off[b + 1];
             const unsigned long long g = gcur[b];
@@ -159,19 +199,17 @@ struct RStageOp {
         // coalesced write-out: srt[i] is entry i + gdel[b] of bucket b's list; the
         // counts are cleared for the next round (nothing reads them until then)
         for (uint32_t b = tid; b <= b_n; b += NW * 64) off[b] = 0u;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
+#pragma unroll KMC_RSCAT_WU
+        for (int q = 0; q < 16 * RT; ++q) {
             const uint32_t i = tid + q * NW * 64;
-            const uint32_t c = i < total ? srt[i] : kNone;
-            if (c == kNone) continue;
+            if (i >= total) break;
+            const uint32_t c = srt[i];
             const long long pos = gdel[(c >> LOW) - b_lo] + (long long)i;
 #if KMC_RSCAT_ABL >= 1
             if (c == 0xFFFFFFFEu)  // diagnostic: never true, keeps the loads
 #endif
             ent[pos] = (uint16_t)(c & ((1u << LOW) - 1));
         }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) code[j] = kNone;
         lds_barrier();  // srt and the counts are free for the next round
     }
 
@@ -217,7 +255,7 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
     __shared__ __attribute__((aligned(16))) unsigned long long lds64[NBK];
     __shared__ int64_t s_first;
     uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds64);
-    constexpr int SB = SCATTER ? NWAVES * 1024 : 1;
+    constexpr int SB = SCATTER ? NWAVES * 1024 * KMC_RSCAT_RT : 1;
     __shared__ __attribute__((aligned(16))) uint32_t s_srt[SB];
     __shared__ uint32_t s_off[SCATTER ? NBK + 1 : 1];
     __shared__ long long s_gdel[SCATTER ? NBK : 1];
@@ -258,11 +296,12 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         if constexpr (SCATTER) {
-            RStageOp<K, NWAVES> op{s_srt, s_off, s_nw, lds64, s_gdel, p.ent, (uint32_t)p.b_lo,
-                                   (uint32_t)(p.b_hi - p.b_lo), wave, lane, tid, {}, {}};
+            using Op = RStageOp<K, NWAVES, KMC_RSCAT_RT>;
+            Op op{s_srt, s_off, s_nw, lds64, s_gdel, p.ent, (uint32_t)p.b_lo, (uint32_t)(p.b_hi - p.b_lo),
+                  wave, lane, tid, 0, {}, {}, {}, {}};
 #pragma unroll
-            for (int j = 0; j < 16; ++j) op.code[j] = RStageOp<K, NWAVES>::kNone;
-            stream_tiles<K, RStageOp<K, NWAVES>, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+            for (int S = 0; S < KMC_RSCAT_RT; ++S) op.wm[S] = 0u;
+            stream_tiles<K, Op, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         } else {
             RCountOp<K> op{lds32};
             stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
