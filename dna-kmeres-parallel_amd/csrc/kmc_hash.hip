@@ -612,7 +612,6 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
 #endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint64_t lt = (1ull << lane) - 1ull;
     for (int i = tid; i < kTableSlots; i += kCountBlock) {
         L.tk[i] = kEmptyH;
         L.tc[i] = 0u;
