@@ -1,27 +1,41 @@
 #!/usr/bin/env python3
 """bench.py — k-mers/s of the dense k-mer counter on synthetic FASTA in HBM.
 
-Workload (BASELINE.json configs[1]): 10 Gbase per GPU as 10 records of 1 Gbase,
-k = 8 (65 536-bin dense histogram), the synthetic layout of SURVEY.md §8(d)
-(uniform iid ACGT from splitmix64, seed 0x5EED0000 + k, one '\\0' after each
-record).  One step = one full pass of the hot path over the batch: count every
-window of every record (kmc_count_dense_ex: histogram kernel + slab reduce +
-spill fix-up; it overwrites every entry of the rank's columns), and, for N > 1,
-zero the other ranks' columns and the RCCL all-reduce of the int32 count matrix
-(records sharded by rank: weak scaling, 10 Gbase per GPU; the N-rank job is one
-10N-Gbase FASTA).  Two count matrices alternate between steps, so that a step's
-all-reduce (async, on RCCL's stream) overlaps the next step's counting; the timed
-region ends after every all-reduce has completed.
+Workload (BASELINE.json metric and configs[1]): one synthetic FASTA of 10
+records x 1 Gbase (10 Gbase), k = 8 (65 536-bin dense histogram), the layout of
+SURVEY.md §8(d): uniform iid ACGT from splitmix64 (seed 0x5EED0000 + k), one
+'\\0' after each record, one global buffer with record r at bytes
+[r*(L+1), (r+1)*(L+1)).
+
+Scaling modes:
+  strong (default) — the 10 Gbase job is cut into N byte ranges by kmc_plan_shards
+      (4 KiB-aligned cuts, a k-1 byte halo past each), as the reference's one
+      launch over the whole buffer (main.cu:290) split N ways; rank r holds only
+      its range + halo in HBM;
+  weak — every rank holds `--records` whole records of its own (C5: 80 Gbase on 8
+      GPUs is `--scaling weak` with 10 records per GPU).
+Either way one step = one full pass of the hot path over the job: every rank
+counts the windows starting in its byte range (kmc_count_dense_ex over the
+global record offsets: histogram kernel + slab reduce + spill fix-up), which
+overwrites all N_rec columns of its int32 count matrix (zeros for records it
+does not touch), then (N > 1) one RCCL all-reduce (sum) of that matrix over
+xGMI.  Two matrices alternate, so a step's async all-reduce overlaps the next
+step's counting; the timed region ends after every all-reduce has completed.
+
+Launch: `python bench.py --gpus N` starts N rank processes itself (before any
+GPU call) when WORLD_SIZE is not set; under torch.distributed.run (one process
+per GPU, WORLD_SIZE/RANK/LOCAL_RANK set) it runs as that rank.
 
 Printed (rank 0, one JSON line): metric/value/unit as BASELINE.json, roofline of
-the histogram kernel (algorithmic bytes = input ASCII bytes + int32 output,
-SURVEY.md §8(d)) timed with HIP events around that kernel on its own stream,
-and the reference CPU path (its own permutationsCountAll compiled from
-/root/reference into oracle/_ref) timed on a bounded sample of the same bytes.
+the histogram kernel (algorithmic bytes = the rank's input ASCII bytes + int32
+output) timed with HIP events around that kernel on its own
+stream, and the reference CPU path (its own permutationsCountAll compiled from
+/root/reference into oracle/_ref) on every host core this process may use.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import threading
 import time
@@ -30,27 +44,145 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "dna-kmeres-parallel_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+SEED_BASE = 0x5EED0000
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=14)  # the clocks settle over ~10 launches
     ap.add_argument("--k", type=int, default=8)
-    ap.add_argument("--records", type=int, default=10, help="records per GPU")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: --records records in total, byte-range shards; weak: --records per GPU")
+    ap.add_argument("--records", type=int, default=10)
     ap.add_argument("--record-len", type=int, default=1_000_000_000, help="bases per record")
-    ap.add_argument("--cpu-sample", type=int, default=64_000_000,
-                    help="bases per CPU thread for the reference CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, available cores)")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="bases per CPU worker for the reference CPU baseline (0 = sized to ~15 s; -1 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_dense_k8_10gbase.json"),
                     help="HBM traffic per launch measured by rocprofv3 --pmc (see profiles/)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launch: N rank processes when no launcher started us
+# ---------------------------------------------------------------------------
+def spawn_ranks(n, argv):
+    """Start n copies of this script as ranks 0..n-1 (env as torch.distributed.run
+    sets it) and return the worst exit status.  Runs before anything touches the
+    GPU: the children are fresh processes, nothing is exec'ed."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, WORLD_SIZE=str(n), RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# the step driver (also run by tests/test_multi.py with gloo and the oracle)
+# ---------------------------------------------------------------------------
+def rank_plan(scaling, world, rank, records, L, k, align=4096):
+    """What rank `rank` of a `world`-rank job counts and holds.
+
+    Returns a dict: n_tot (records of the job), indices (global int64 offsets,
+    n_tot + 1), win = (win_lo, win_hi) (windows starting there are this rank's),
+    read = (read_lo, read_hi) (bytes the count reads: the range + its k-1 halo),
+    base (global offset of the rank's buffer start, read_lo rounded down to 16 so
+    the library's data pointer stays aligned), hold = (base, read_hi)."""
+    import numpy as np
+
+    import kmc
+    if scaling == "strong":
+        n_tot = records
+        idx = kmc.synth_indices(n_tot, L)
+        win_lo, win_hi, read_lo, read_hi = kmc.plan_shards(idx, k, world, align)[rank]
+    elif scaling == "weak":
+        n_tot = records * world
+        idx = kmc.synth_indices(n_tot, L)
+        win_lo, win_hi = int(idx[rank * records]), int(idx[(rank + 1) * records])
+        read_lo, read_hi = win_lo, win_hi  # whole records: the last byte is a terminator, no halo
+    else:
+        raise ValueError(scaling)
+    base = int(read_lo) & ~15
+    return {"n_tot": n_tot, "indices": np.asarray(idx, dtype=np.int64), "win": (int(win_lo), int(win_hi)),
+            "read": (int(read_lo), int(read_hi)), "base": base, "hold": (base, int(read_hi))}
+
+
+def overlapped_steps(bufs, count, world, all_reduce):
+    """step(i) counts into bufs[i % len(bufs)] (count(j) overwrites every entry of
+    matrix j: this rank's counts, zeros for records it does not touch) and, for
+    world > 1, starts the matrix's all-reduce without waiting for it
+    (all_reduce(t, async_op=True)), so that it overlaps the next step, which uses
+    the other matrix; a matrix is reused only after its previous all-reduce is
+    done.  drain() waits for every pending all-reduce."""
+    nbuf = len(bufs)
+    pending = [None] * nbuf  # the all-reduce last issued on each matrix
+
+    def step(i):
+        j = i % nbuf
+        if pending[j] is not None:
+            pending[j].wait()  # stream-ordered on RCCL: the previous all-reduce of this matrix
+            pending[j] = None
+        count(j)
+        if world > 1:
+            pending[j] = all_reduce(bufs[j], async_op=True)
+        return j
+
+    def drain():
+        for j in range(nbuf):
+            if pending[j] is not None:
+                pending[j].wait()
+                pending[j] = None
+
+    return step, drain
+
+
+def host_kmer_hist(bases, k):
+    """numpy histogram of the windows of one all-ACGT byte run (LE bin order:
+    the first base is the least significant digit, utils.h:35-47)."""
+    import numpy as np
+    lut = np.zeros(256, dtype=np.int64)
+    lut[np.frombuffer(b"ACGT", dtype=np.uint8)] = np.arange(4)
+    c = lut[bases]
+    nw = c.size - k + 1
+    code = np.zeros(nw, dtype=np.int64)
+    for p in range(k):
+        code |= c[p:p + nw] << (2 * p)
+    return np.bincount(code, minlength=1 << (2 * k))
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's permutationsCountAll on the host cores
+# ---------------------------------------------------------------------------
+def usable_cores():
+    """(cores this process may run on: affinity capped by the cgroup CPU quota,
+    CPUs of the machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n, os.cpu_count() or n
 
 
 def cpu_baseline(host_bytes_list, k, threads):
     """Reference CPU path (permutationsCountAll, main.cu:636-646) on `threads`
-    disjoint samples in parallel; returns (kmers/s, kind, detail)."""
+    disjoint samples in parallel (ctypes drops the GIL); returns (kmers/s, kind,
+    seconds, kmers)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle
@@ -81,37 +213,52 @@ def cpu_baseline(host_bytes_list, k, threads):
     return kmers / dt, kind, dt, kmers
 
 
-def overlapped_steps(bufs, count, world, all_reduce):
-    """step(i) counts into bufs[i % len(bufs)] (count(j): this rank's columns) and,
-    for world > 1, zeroes the matrix first and starts its all-reduce without
-    waiting for it (all_reduce(t, async_op=True)), so that it overlaps the next
-    step, which uses the other matrix; a matrix is reused only after its previous
-    all-reduce is done.  drain() waits for every pending all-reduce."""
-    nbuf = len(bufs)
-    pending = [None] * nbuf  # the all-reduce last issued on each matrix
-
-    def step(i):
-        j = i % nbuf
-        if world > 1:
-            if pending[j] is not None:
-                pending[j].wait()  # stream-ordered on RCCL: the previous all-reduce of this matrix
-            bufs[j].zero_()  # the other ranks' columns, before the summing all-reduce
-        count(j)
-        if world > 1:
-            pending[j] = all_reduce(bufs[j], async_op=True)
-        return j
-
-    def drain():
-        for j in range(nbuf):
-            if pending[j] is not None:
-                pending[j].wait()
-                pending[j] = None
-
-    return step, drain
+def cpu_model():
+    import platform
+    m = platform.processor()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return m
 
 
+def run_cpu_baseline(args, data, L, k, n_rec):
+    import numpy as np
+    threads, node_cpus = usable_cores()
+    if args.cpu_threads:
+        threads = args.cpu_threads
+    # one thread first: its rate sizes the per-worker sample to ~15 s of work
+    probe = np.append(data[: 4_000_000].cpu().numpy(), np.uint8(0))
+    rate1, kind, dt1, _ = cpu_baseline([probe], k, 1)
+    S = args.cpu_sample or int(min(max(rate1 * 15.0, 1e6), 256e6))
+    host = []
+    for t in range(threads):
+        r = t % n_rec
+        off = r * (L + 1) + ((t // n_rec) * S) % max(L - S, 1)
+        host.append(np.append(data[off: off + S].cpu().numpy(), np.uint8(0)))  # one record of S bases
+    rate, kind, dt, kmers = cpu_baseline(host, k, threads)
+    return {
+        "value": rate, "unit": "k-mers/s", "cores": threads, "kind": kind,
+        "value_1thread": rate1, "node_cpus": node_cpus,
+        "sample": "%d workers x %d bases of the same synthetic records (%.1f s wall, %d k-mers), k=%d, the "
+                  "reference's permutationsCountAll (substr + std::map, main.cu:636-646) built -O2 from "
+                  "/root/reference; cores = the CPUs this process may use (affinity and cgroup quota; the "
+                  "machine shows %d); value_1thread: 1 worker x %d bases (%.1f s); CPU: %s"
+                  % (threads, S, dt, kmers, k, node_cpus, probe.size - 1, dt1, cpu_model()),
+    }
+
+
+# ---------------------------------------------------------------------------
 def main():
-    args = parse()
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, argv))
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -123,33 +270,43 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # KMC_BENCH_BACKEND=gloo: rehearsal of the N-rank path with every rank on the
+    # one GPU of a test box (RCCL needs one device per rank); never a measurement
+    backend = os.environ.get("KMC_BENCH_BACKEND", "nccl")
+    local = local % torch.cuda.device_count() if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     k = args.k
     nb = 1 << (2 * k)
-    n_loc, L = args.records, args.record_len
-    n_tot = n_loc * world
-    seed = 0x5EED0000 + k
-    data_bytes = n_loc * (L + 1)
-    # this rank's records are records [rank*n_loc, (rank+1)*n_loc) of one global
-    # FASTA whose base stream is continuous across records
-    data = torch.empty(data_bytes, dtype=torch.uint8, device=dev)
-    kmc.synth_fill(data, n_loc, L, seed, first_base=rank * n_loc * L)
-    idx = torch.from_numpy(kmc.synth_indices(n_loc, L)).to(dev)
-    # count matrices sum[s_global + n_tot*code]; with N > 1 two of them, so that a
-    # step's all-reduce (RCCL, its own stream) overlaps the next step's counting
+    L = args.record_len
+    seed = SEED_BASE + k
+    plan = rank_plan(args.scaling, world, rank, args.records, L, k)
+    n_tot = plan["n_tot"]
+    base, hold_hi = plan["hold"]
+    (win_lo, win_hi), (read_lo, read_hi) = plan["win"], plan["read"]
+    # this rank's bytes of the one global buffer (its byte range + halo), generated in HBM
+    data = torch.empty(max(hold_hi - base, 16), dtype=torch.uint8, device=dev)
+    kmc.synth_fill_range(data, base, hold_hi, L, seed)
+    idx = torch.from_numpy(plan["indices"]).to(dev)
     nbuf = 2 if world > 1 else 1
-    bufs = [torch.zeros((nb, n_tot), dtype=torch.int32, device=dev) for _ in range(nbuf)]
-    a0 = kmc.dense_args(data, idx, k, bufs[0].view(-1)[rank * n_loc:], ld=n_tot)
-    ws = torch.empty(kmc.dense_ex_workspace_size(a0, local), dtype=torch.uint8, device=dev)
-    args_b = [kmc.dense_args(data, idx, k, b.view(-1)[rank * n_loc:], ld=n_tot, workspace=ws) for b in bufs]
+    bufs = [torch.empty((nb, n_tot), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+
+    def dargs(out, ws=None):
+        return kmc.dense_args(data, idx, k, out.view(-1), read=(read_lo, read_hi), win=(win_lo, win_hi),
+                              workspace=ws, data_offset=base)
+
+    ws = torch.empty(max(kmc.dense_ex_workspace_size(dargs(bufs[0]), local), 1), dtype=torch.uint8, device=dev)
+    args_b = [dargs(b, ws) for b in bufs]
     stream = torch.cuda.current_stream()
 
     def count(j):
-        kmc.count_dense_ex(args_b[j], stream)  # overwrites every entry of this rank's columns
+        kmc.count_dense_ex(args_b[j], stream)  # overwrites every entry of the matrix
 
     step, drain = overlapped_steps(bufs, count, world, dist.all_reduce if world > 1 else None)
 
@@ -168,10 +325,22 @@ def main():
     drain()
     torch.cuda.synchronize()
     if args.warmup > 0:
-        # every window of the synthetic input is valid, so each record's column sums to L-k+1
+        # (1) every window of the synthetic input is valid: after the all-reduce each
+        # record's column sums to L-k+1; (2) bins, not only totals: a 1 Mbase slice of
+        # this rank's bytes counted as a record of its own equals a numpy histogram of
+        # the same bytes regenerated on the host
         tot = bufs[last].to(torch.int64).sum(dim=0)
         if not bool((tot == (L - k + 1)).all()):
             raise SystemExit("count check failed: column sums %s" % tot[:4].tolist())
+        s_lo = win_lo - base
+        s_len = min(1 << 20, L - (win_lo % (L + 1)), max(win_hi - win_lo, 0))
+        if s_len >= k:
+            sl = torch.zeros(s_len + 16, dtype=torch.uint8, device=dev)
+            sl[:s_len] = data[s_lo:s_lo + s_len]
+            got, _ = kmc.count_dense(sl, torch.tensor([0, s_len + 1], dtype=torch.int64, device=dev), k)
+            exp = host_kmer_hist(kmc.synth_host_range(win_lo, win_lo + s_len, L, seed), k)
+            if not np.array_equal(got.view(-1).cpu().numpy().astype(np.int64), exp):
+                raise SystemExit("count check failed: a 1 Mbase slice differs from its host histogram")
     for i in range(args.warmup - n_after, args.warmup):
         step(i)
     drain()
@@ -189,27 +358,30 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     kmc.trace_events(None, None)
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    kern_ms = torch.tensor([sum(b.elapsed_time(e) for b, e in ev) / args.steps], dtype=torch.float64, device=dev)
+    # algorithmic bytes of one histogram launch on this GPU: its ASCII input bytes +
+    # the int32 matrix it writes
+    alg_bytes = (win_hi - win_lo) + 4 * nb * n_tot
+    kern_ms = sum(b.elapsed_time(e) for b, e in ev) / args.steps
+    stats = torch.tensor([t1 - t0, kern_ms, -alg_bytes / (kern_ms * 1e-3) / 1e9], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kern_ms, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
-    kern_ms = float(kern_ms.item())
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms, achieved = float(stats[0]), float(stats[1]), -float(stats[2])  # max, max, min over ranks
 
     kmers_per_step = n_tot * (L - k + 1)
     value = kmers_per_step * args.steps / elapsed
-    # algorithmic bytes of one histogram launch on one GPU: ASCII input incl.
-    # terminators + int32 output of this rank's records
-    alg_bytes = data_bytes + 4 * nb * n_loc
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
-    if os.path.exists(args.pmc):
+    if world == 1 and os.path.exists(args.pmc):
         with open(args.pmc) as f:
             pmc = json.load(f)
-        if pmc.get("k") == k and pmc.get("data_bytes") == data_bytes:
+        if pmc.get("k") == k and pmc.get("data_bytes") == win_hi - win_lo:
             traffic = pmc.get("hbm_bytes_per_launch")
 
+    if args.scaling == "strong":
+        par = ("one %.1f Gbase buffer cut into %d byte-range shard(s) (kmc_plan_shards, 4 KiB cuts, k-1 halo), "
+               "RCCL all-reduce of the int32 count matrix overlapping the next step" % (n_tot * L / 1e9, world))
+    else:
+        par = ("%d records per GPU, RCCL all-reduce of the int32 count matrix overlapping the next step"
+               % args.records)
     result = {
         "metric": "k-mers/sec (whole node), 10 Gbase synthetic FASTA, at 1/2/4/8 MI355X",
         "value": value,
@@ -219,16 +391,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 uniform ACGT generated in HBM; SURVEY.md 8(d) layout)",
         "config": {
-            "workload": "dense k=%d histogram, %d records x %d bases per GPU (%.1f Gbase per GPU)"
-                        % (k, n_loc, L, n_loc * L / 1e9),
-            "k": k, "records_per_gpu": n_loc, "record_len": L, "total_records": n_tot,
-            "bins": nb, "parallelism": "records sharded over %d GPU(s), RCCL all-reduce of int32 counts "
-                                       "(overlapping the next step)" % world,
+            "workload": "dense k=%d histogram, %d records x %d bases (%.1f Gbase) in total, %s"
+                        % (k, n_tot, L, n_tot * L / 1e9,
+                           "split over the GPUs" if args.scaling == "strong" else "%d records per GPU" % args.records),
+            "k": k, "total_records": n_tot, "record_len": L, "bins": nb, "parallelism": par,
         },
         "roofline": {
             "bound": "hbm",
@@ -237,44 +408,17 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
-            "kernel": "count_dense_kernel<8> (HIP events around the histogram launch)",
+            "kernel": "count_dense_kernel<%d> (HIP events around the histogram launch; slowest rank)" % k,
             "kernel_ms": kern_ms,
             "alg_bytes_per_launch": alg_bytes,
         },
     }
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        S = args.cpu_sample
-        host = []
-        for t in range(threads):
-            r = t % n_loc
-            off = r * (L + 1) + (t // n_loc) * S
-            chunk = data[off: off + S].cpu().numpy()
-            host.append(np.append(chunk, np.uint8(0)))  # one record of S bases + terminator
-        rate, kind, dt, kmers = cpu_baseline(host, k, threads)
-        # the same code on one thread (a quarter of one sample)
-        one = [np.append(host[0][: max(S // 4, k + 1)], np.uint8(0))]
-        rate1, _, dt1, _ = cpu_baseline(one, k, 1)
-        import platform
-        cpu_model = platform.processor()
-        try:
-            with open("/proc/cpuinfo") as f:
-                for line in f:
-                    if line.startswith("model name"):
-                        cpu_model = line.split(":", 1)[1].strip()
-                        break
-        except OSError:
-            pass
-        result["cpu_baseline"] = {
-            "value": rate, "unit": "k-mers/s", "cores": threads, "kind": kind,
-            "value_1thread": rate1,
-            "sample": "%d threads x %d bases of the same synthetic records (%.0f s wall, %d k-mers), "
-                      "k=%d, permutationsCountAll (substr + std::map, main.cu:636-646) -O2; value_1thread: "
-                      "1 thread x %d bases (%.1f s); CPU: %s"
-                      % (threads, S, dt, kmers, k, one[0].size - 1, dt1, cpu_model),
-        }
+    if rank == 0 and world == 1 and args.cpu_sample >= 0:
+        result["cpu_baseline"] = run_cpu_baseline(args, data, L, k, n_tot)
+    if backend != "nccl":
+        result["rehearsal"] = "KMC_BENCH_BACKEND=%s, %d ranks sharing device(s): not a measurement" % (backend, world)
     if rank == 0:
-        print(json.dumps(result))
+        print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -14,14 +14,16 @@
 namespace kmc {
 namespace {
 
-__global__ __launch_bounds__(256) void synth_kernel(char *data, uint64_t total, uint64_t rec_bytes,
+// data[b] = global byte start + b of the record stream (record r at r*rec_bytes),
+// b < total.
+__global__ __launch_bounds__(256) void synth_kernel(char *data, uint64_t total, uint64_t start, uint64_t rec_bytes,
                                                     uint64_t record_len, uint64_t seed, uint64_t first_base) {
     const uint64_t nchunks = (total + 15) / 16;
     for (uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; ch < nchunks;
          ch += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t b0 = ch * 16;
-        uint64_t r = b0 / rec_bytes;
-        uint64_t off = b0 - r * rec_bytes;
+        uint64_t r = (start + b0) / rec_bytes;
+        uint64_t off = (start + b0) - r * rec_bytes;
         uint64_t cached_n = ~0ull, word = 0;
         uint32_t v[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -53,6 +55,16 @@ __global__ __launch_bounds__(256) void synth_kernel(char *data, uint64_t total, 
     }
 }
 
+int launch_synth(char *data, uint64_t total, uint64_t start, uint64_t record_len, uint64_t seed,
+                 uint64_t first_base, hipStream_t stream) {
+    const uint64_t nchunks = (total + 15) / 16;
+    uint64_t blocks = (nchunks + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, data, total, start,
+                       record_len + 1, record_len, seed, first_base);
+    return (int)hipGetLastError();
+}
+
 }  // namespace
 }  // namespace kmc
 
@@ -61,14 +73,16 @@ extern "C" int kmc_synth_fill(char *data, uint64_t num_records, uint64_t record_
     if (num_records == 0) return KMC_OK;
     if (!data) return KMC_ERR_INVALID_ARG;
     if (reinterpret_cast<uintptr_t>(data) & 15u) return KMC_ERR_ALIGNMENT;
-    const uint64_t rec_bytes = record_len + 1;
-    const uint64_t total = num_records * rec_bytes;
-    const uint64_t nchunks = (total + 15) / 16;
-    uint64_t blocks = (nchunks + 255) / 256;
-    if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(kmc::synth_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, data, total, rec_bytes,
-                       record_len, seed, first_base);
-    return (int)hipGetLastError();
+    return kmc::launch_synth(data, num_records * (record_len + 1), 0, record_len, seed, first_base, stream);
+}
+
+extern "C" int kmc_synth_fill_range(char *data, uint64_t lo, uint64_t hi, uint64_t record_len, uint64_t seed,
+                                    hipStream_t stream) {
+    if (hi < lo) return KMC_ERR_INVALID_ARG;
+    if (hi == lo) return KMC_OK;
+    if (!data) return KMC_ERR_INVALID_ARG;
+    if (reinterpret_cast<uintptr_t>(data) & 15u) return KMC_ERR_ALIGNMENT;
+    return kmc::launch_synth(data, hi - lo, lo, record_len, seed, 0, stream);
 }
 
 extern "C" void kmc_synth_indices(int64_t *indices, uint64_t num_records, uint64_t record_len) {

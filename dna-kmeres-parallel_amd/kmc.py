@@ -75,6 +75,7 @@ def lib():
         L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
         L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.kmc_synth_fill.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
+        L.kmc_synth_fill_range.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
         L.kmc_synth_indices.argtypes = [_P, _U64, _U64]
         L.kmc_synth_indices.restype = None
         L.kmc_fasta_load.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P)]
@@ -260,6 +261,12 @@ def synth_fill(data, num_records, record_len, seed, first_base=0, stream=None):
     _check(rc, "kmc_synth_fill")
 
 
+def synth_fill_range(data, lo, hi, record_len, seed, stream=None):
+    """Global bytes [lo, hi) of the synthetic record stream into data[0 .. hi-lo)."""
+    rc = lib().kmc_synth_fill_range(_dptr(data), lo, hi, record_len, seed, _stream(stream))
+    _check(rc, "kmc_synth_fill_range")
+
+
 def synth_indices(num_records, record_len):
     out = np.zeros(num_records + 1, dtype=np.int64)
     lib().kmc_synth_indices(out.ctypes.data_as(_P), num_records, record_len)
@@ -390,6 +397,19 @@ def splitmix64_np(seed, n):
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         return z ^ (z >> np.uint64(31))
+
+
+def synth_host_range(lo, hi, record_len, seed):
+    """Same bytes as kmc_synth_fill_range, on the host (small sizes)."""
+    p = np.arange(lo, hi, dtype=np.uint64)
+    rb = np.uint64(record_len + 1)
+    r, off = p // rb, p % rb
+    g = r * np.uint64(record_len) + off
+    words = splitmix64_np(seed, g >> np.uint64(5))
+    codes = ((words >> (np.uint64(2) * (g & np.uint64(31)))) & np.uint64(3)).astype(np.uint8)
+    out = np.frombuffer(b"ACGT", dtype=np.uint8)[codes]
+    out[off == np.uint64(record_len)] = 0
+    return out
 
 
 def synth_host(num_records, record_len, seed, first_base=0):

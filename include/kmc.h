@@ -219,6 +219,13 @@ int kmc_trace_set_events(hipEvent_t before, hipEvent_t after);
 int kmc_synth_fill(char *data, uint64_t num_records, uint64_t record_len, uint64_t seed,
                    uint64_t first_base, hipStream_t stream);
 void kmc_synth_indices(int64_t *indices, uint64_t num_records, uint64_t record_len);
+/* Bytes [lo, hi) of the same record stream with first_base = 0 (record r occupies
+ * global bytes [r*(record_len+1), (r+1)*(record_len+1)), its last one '\0'),
+ * written to data[0 .. hi-lo): what a rank of a strong-scaled job holds of the
+ * one global buffer (its shard and halo) without generating whole records.
+ * data 16-byte aligned; lo need not be. */
+int kmc_synth_fill_range(char *data, uint64_t lo, uint64_t hi, uint64_t record_len, uint64_t seed,
+                         hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* FASTA loader (host), the successor of importSeqs / importSeqsNoNL

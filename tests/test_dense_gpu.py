@@ -350,3 +350,54 @@ def test_count_multi_single_device(kmc, oracle, cuda):
     exp, exp_inv = oracle.count_dense(data, idx, 5)
     np.testing.assert_array_equal(got, exp)
     np.testing.assert_array_equal(inv, exp_inv)
+
+
+def test_synth_fill_range_matches_host(kmc, cuda):
+    """kmc_synth_fill_range (a rank's byte range of the one global buffer) equals
+    the same bytes of the whole-record generator, for unaligned and record-cutting
+    ranges."""
+    import torch
+    L, seed = 4093, 0x5EED0008
+    for lo, hi in ((0, 5 * 4094), (1, 4095), (4093, 4094), (4100, 13_000), (3 * 4094 - 5, 5 * 4094)):
+        buf = torch.zeros(hi - lo + 64, dtype=torch.uint8, device=cuda)
+        kmc.synth_fill_range(buf, lo, hi, L, seed)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(buf[:hi - lo].cpu().numpy(), kmc.synth_host_range(lo, hi, L, seed))
+        assert int(buf[hi - lo:].sum()) == 0
+
+
+@pytest.mark.parametrize("scaling,world,records,L,k", [
+    ("strong", 2, 4, 3_000_000, 8),
+    ("strong", 8, 3, 2_000_000, 8),
+    ("strong", 4, 3, 1_500_000, 11),
+    ("strong", 4, 3, 1_000, 8),      # three of the four shards are empty
+    ("weak", 4, 2, 1_000_000, 8),
+])
+def test_bench_rank_counts_sum_to_whole(kmc, oracle, cuda, scaling, world, records, L, k):
+    """bench.py's per-rank step on the GPU: each rank holds only its byte range +
+    halo (kmc_synth_fill_range) and counts its window range into all columns of
+    its matrix; the ranks' matrices sum to the oracle's histogram of the whole
+    buffer (the all-reduce is a plain integer sum: tests/test_multi.py)."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    seed = bench.SEED_BASE + k
+    acc = None
+    for r in range(world):
+        p = bench.rank_plan(scaling, world, r, records, L, k)
+        base, hold_hi = p["hold"]
+        data = torch.empty(max(hold_hi - base, 16), dtype=torch.uint8, device=cuda)
+        kmc.synth_fill_range(data, base, hold_hi, L, seed)
+        idx = torch.from_numpy(p["indices"]).to(cuda)
+        out = torch.full((1 << (2 * k), p["n_tot"]), -5, dtype=torch.int32, device=cuda)
+        kmc.count_dense_ex(kmc.dense_args(data, idx, k, out.view(-1), read=p["read"], win=p["win"],
+                                          data_offset=base))
+        torch.cuda.synchronize()
+        part = out.cpu().numpy().astype(np.int64)
+        acc = part if acc is None else acc + part
+        del out, data
+    total = int(p["indices"][-1])
+    exp, _ = oracle.count_dense(kmc.synth_host_range(0, total, L, seed), p["indices"], k)
+    np.testing.assert_array_equal(acc, exp)

@@ -99,9 +99,9 @@ def test_gloo_world2_shard_allreduce(k):
 
 def _overlap_worker(rank, world, port, steps, q):
     """bench.py's overlapped steps with a CPU stand-in for the count: each step
-    writes rank- and step-specific values into this rank's columns; after the
-    async gloo all-reduces every matrix must hold the sum over ranks of its last
-    step's columns."""
+    overwrites the whole matrix (rank- and step-specific values in this rank's
+    columns, zeros elsewhere, as kmc_count_dense_ex does); after the async gloo
+    all-reduces every matrix must hold the sum over ranks of its last step."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.dirname(here))
@@ -117,8 +117,9 @@ def _overlap_worker(rank, world, port, steps, q):
     bufs = [torch.full((nb, n_tot), -7, dtype=torch.int32) for _ in range(2)]
     last_step = [None, None]
 
-    def count(j):  # this rank's columns only, every entry overwritten
+    def count(j):
         i = last_step[j]
+        bufs[j].zero_()
         cols = torch.arange(n_loc, dtype=torch.int32) + rank * n_loc
         bufs[j][:, rank * n_loc:(rank + 1) * n_loc] = (i * 1000 + cols)[None, :] + torch.arange(nb, dtype=torch.int32)[:, None]
 
@@ -137,15 +138,121 @@ def _overlap_worker(rank, world, port, steps, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_bench_overlapped_allreduce():
+def _spawn(target, world, *args):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, 7, q)) for r in range(2)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
+    return res
+
+
+def test_gloo_world2_bench_overlapped_allreduce():
+    res = _spawn(_overlap_worker, 2, 7)
     assert all(ok for _, ok in res), res
+
+
+def _bench_step_worker(rank, world, port, scaling, records, L, k, steps, q):
+    """bench.py's step driver exactly as the GPU run uses it (rank_plan: which
+    bytes a rank holds and which windows it counts; overlapped_steps: count, then
+    the async all-reduce), with the rank's bytes generated on the host
+    (synth_host_range, the twin of kmc_synth_fill_range) and the oracle as the
+    counter over the rank's window range of the global offsets."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [repo, os.path.join(repo, "dna-kmeres-parallel_amd"), os.path.join(repo, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import kmc
+    import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seed = bench.SEED_BASE + k
+    plan = bench.rank_plan(scaling, world, rank, records, L, k)
+    n_tot, idx = plan["n_tot"], plan["indices"]
+    base, hold_hi = plan["hold"]
+    win_lo, win_hi = plan["win"]
+    read_lo, read_hi = plan["read"]
+    held = kmc.synth_host_range(base, hold_hi, L, seed)
+    # the oracle indexes the global buffer: the held bytes go to their global
+    # offsets and every other byte is 'A', so a count that read outside
+    # [read_lo, read_hi) would show
+    total = int(idx[-1])
+    glob = np.full(total, ord("A"), dtype=np.uint8)
+    glob[read_lo:read_hi] = held[read_lo - base:read_hi - base]
+    bufs = [torch.full((1 << (2 * k), n_tot), -1, dtype=torch.int32) for _ in range(2)]
+
+    def count(j):
+        part, _ = oracle.count_dense(glob, idx, k, win=(win_lo, win_hi))
+        bufs[j].copy_(torch.from_numpy(part))
+
+    step, drain = bench.overlapped_steps(bufs, count, world, dist.all_reduce)
+    for i in range(steps):
+        step(i)
+    drain()
+    full, _ = oracle.count_dense(kmc.synth_host_range(0, total, L, seed), idx, k)
+    ok = all(bool(np.array_equal(b.numpy(), full)) for b in bufs[:min(steps, 2)])
+    sums_ok = bool((bufs[0].to(torch.int64).sum(dim=0) == L - k + 1).all())
+    q.put((rank, ok, sums_ok, (win_lo, win_hi)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,scaling,records,L,k", [
+    (2, "strong", 5, 9_000, 8),   # shard cuts inside records
+    (4, "strong", 5, 9_000, 4),
+    (4, "strong", 3, 1_000, 3),   # 3003 bytes < one 4 KiB cut: three empty shards
+    (2, "weak", 3, 5_000, 8),
+    (4, "weak", 2, 3_000, 5),
+])
+def test_gloo_bench_step_driver(world, scaling, records, L, k):
+    res = _spawn(_bench_step_worker, world, scaling, records, L, k, 3)
+    assert all(ok and sums for _, ok, sums, _ in res), res
+    wins = sorted(w for *_, w in res)
+    # the ranks' window ranges tile the job's buffer exactly
+    assert wins[0][0] == 0 and all(a[1] == b[0] for a, b in zip(wins, wins[1:]))
+    n_tot = records if scaling == "strong" else records * world
+    assert wins[-1][1] == n_tot * (L + 1)
+
+
+def test_bench_rank_plan_single_gpu_is_whole_buffer(kmc):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for scaling in ("strong", "weak"):
+        p = bench.rank_plan(scaling, 1, 0, 10, 1_000_000_000, 8)
+        assert p["n_tot"] == 10 and p["win"] == (0, 10 * 1_000_000_001) and p["read"] == p["win"]
+        assert p["hold"] == (0, 10 * 1_000_000_001)
+    # 8-way strong plan of the 10 Gbase job: 4 KiB-aligned cuts, halo k-1, 16-aligned buffers
+    plans = [bench.rank_plan("strong", 8, r, 10, 1_000_000_000, 8) for r in range(8)]
+    for r, p in enumerate(plans):
+        lo, hi = p["win"]
+        assert p["read"] == (lo, min(hi + 7, 10 * 1_000_000_001)) and p["base"] % 16 == 0
+        if r:
+            assert lo % 4096 == 0 and plans[r - 1]["win"][1] == lo
+        assert abs((hi - lo) - 1_250_000_001) <= 4096
+
+
+def test_synth_host_range_matches_whole_records(kmc):
+    whole = kmc.synth_host(4, 1000, seed=0x5EED0008)
+    for lo, hi in [(0, 4004), (1, 17), (999, 1003), (1000, 1001), (2500, 4004), (7, 7)]:
+        np.testing.assert_array_equal(kmc.synth_host_range(lo, hi, 1000, 0x5EED0008), whole[lo:hi])
+
+
+def test_bench_host_histogram_matches_oracle(oracle):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import kmc as _k
+    b = _k.synth_host_range(123, 123 + 50_000, 1_000_000, 0x5EED0008)
+    for k in (1, 5, 8):
+        exp, _ = oracle.count_dense(np.append(b, np.uint8(0)), np.array([0, b.size + 1], dtype=np.int64), k)
+        np.testing.assert_array_equal(bench.host_kmer_hist(b, k), exp[:, 0])
