@@ -26,8 +26,10 @@
 //            recorded as a spill entry and re-added by spill_apply_kernel.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -499,30 +501,33 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     }
 }
 
-// Records that span several workgroups: sum their slab slots.
+// Records that span several workgroups: sum their slab slots; records without a
+// window in range get zeros.  Grid (ceil(4^k / 256), ny): blockIdx.x picks 256
+// codes, records s = blockIdx.y, blockIdx.y + ny, ... (the record count is not
+// bounded by the grid: gridDim.x * blockDim.x stays far below 2^32).
 template <int K, class Idx>
 __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     constexpr int NB = 1 << (2 * K);
-    constexpr int CB = (NB + 255) / 256;
-    const int64_t s = blockIdx.x / CB;
-    const int c = (int)(blockIdx.x % CB) * 256 + threadIdx.x;
-    if (s >= p.n || c >= NB) return;
+    const int c = (int)blockIdx.x * 256 + threadIdx.x;
+    if (c >= NB) return;
     const Geom g = make_geom<Idx>(p);
-    int64_t ca, ce;
-    record_windows<K, Idx>(p, g, s, ca, ce);
-    if (ce <= ca) {
-        p.sum[s + p.ld * (int64_t)c] = 0;
-        return;
+    for (int64_t s = blockIdx.y; s < p.n; s += gridDim.y) {
+        int64_t ca, ce;
+        record_windows<K, Idx>(p, g, s, ca, ce);
+        if (ce <= ca) {
+            p.sum[s + p.ld * (int64_t)c] = 0;
+            continue;
+        }
+        const int64_t wf = ((ca >> kTileShift) - g.T0) / g.tpw;
+        const int64_t wlast = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
+        if (wf == wlast) continue;  // written directly by the count kernel
+        uint32_t acc = 0;
+        for (int64_t w = wf; w <= wlast; ++w) {
+            if (p.slot_rec[2 * w] == s) acc += p.slab[(2 * w) * NB + c];
+            if (p.slot_rec[2 * w + 1] == s) acc += p.slab[(2 * w + 1) * NB + c];
+        }
+        p.sum[s + p.ld * (int64_t)c] = (int32_t)acc;
     }
-    const int64_t wf = ((ca >> kTileShift) - g.T0) / g.tpw;
-    const int64_t wlast = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
-    if (wf == wlast) return;  // written directly by the count kernel
-    uint32_t acc = 0;
-    for (int64_t w = wf; w <= wlast; ++w) {
-        if (p.slot_rec[2 * w] == s) acc += p.slab[(2 * w) * NB + c];
-        if (p.slot_rec[2 * w + 1] == s) acc += p.slab[(2 * w + 1) * NB + c];
-    }
-    p.sum[s + p.ld * (int64_t)c] = (int32_t)acc;
 }
 
 __global__ __launch_bounds__(256) void spill_apply_kernel(Params p) {
@@ -536,27 +541,29 @@ __global__ __launch_bounds__(256) void spill_apply_kernel(Params p) {
     }
 }
 
-// invalid[s] = (#windows of s in range) - sum over codes (the CPU path's bin 0).
+// invalid[s] = (#windows of s in range) - sum over codes (the CPU path's bin 0);
+// records blockIdx.x, blockIdx.x + gridDim.x, ...
 template <int K, class Idx>
 __global__ __launch_bounds__(256) void invalid_kernel(Params p) {
     constexpr int NB = 1 << (2 * K);
-    const int64_t s = blockIdx.x;
-    if (s >= p.n) return;
-    int64_t acc = 0;
-    for (int c = threadIdx.x; c < NB; c += 256) acc += p.sum[s + p.ld * (int64_t)c];
     __shared__ int64_t red[256];
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    for (int64_t s = blockIdx.x; s < p.n; s += gridDim.x) {
+        int64_t acc = 0;
+        for (int c = threadIdx.x; c < NB; c += 256) acc += p.sum[s + p.ld * (int64_t)c];
+        red[threadIdx.x] = acc;
         __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const Geom g = make_geom<Idx>(p);
-        int64_t ca, ce;
-        record_windows<K, Idx>(p, g, s, ca, ce);
-        const int64_t nw = ce > ca ? ce - ca : 0;
-        p.invalid[s] = (int32_t)(nw - red[0]);
+        for (int st = 128; st > 0; st >>= 1) {
+            if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            const Geom g = make_geom<Idx>(p);
+            int64_t ca, ce;
+            record_windows<K, Idx>(p, g, s, ca, ce);
+            const int64_t nw = ce > ca ? ce - ca : 0;
+            p.invalid[s] = (int32_t)(nw - red[0]);
+        }
+        __syncthreads();  // red is reused by the next record
     }
 }
 
@@ -627,6 +634,14 @@ int grid_size(int device, int &G) {
     }
     G = d.cus * d.occ[K][ix];
     return 0;
+}
+
+bool check_spill() {
+    static const bool on = [] {
+        const char *e = std::getenv("KMC_CHECK_SPILL");
+        return e != nullptr && e[0] == '1';
+    }();
+    return on;
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -797,17 +812,31 @@ int run_dense(const Request &q, hipStream_t st) {
         he = hipGetLastError();
         if (he != hipSuccess) return (int)he;
     }
-    const int64_t cb = (NB + 255) / 256;
-    hipLaunchKernelGGL((reduce_dense_kernel<K, Idx>), dim3((unsigned)(q.n * cb)), dim3(256), 0, st, p);
+    const unsigned cb = (unsigned)((NB + 255) / 256);
+    hipLaunchKernelGGL((reduce_dense_kernel<K, Idx>), dim3(cb, (unsigned)std::min<int64_t>(q.n, kMaxGridY)), dim3(256),
+                       0, st, p);
     he = hipGetLastError();
     if (he != hipSuccess) return (int)he;
     if (Cfg<K>::P16) {
         hipLaunchKernelGGL(spill_apply_kernel, dim3(pl.G), dim3(256), 0, st, p);
         he = hipGetLastError();
         if (he != hipSuccess) return (int)he;
+        // spill_cap_for bounds the entries a workgroup can emit (scan entries stand
+        // for >= 32 768 windows, wrap entries for 65 536, at most 3 per wrap), and
+        // p16_spill keeps counting past the cap; with KMC_CHECK_SPILL=1 (tests) the
+        // call synchronises and fails instead of returning counts that lost entries
+        if (check_spill()) {
+            std::vector<uint32_t> cnt(pl.G);
+            he = hipMemcpyAsync(cnt.data(), p.spill_cnt, pl.G * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+            if (he == hipSuccess) he = hipStreamSynchronize(st);
+            if (he != hipSuccess) return (int)he;
+            for (uint32_t c : cnt)
+                if (c > pl.spill_cap) return KMC_ERR_CAPACITY;
+        }
     }
     if (q.invalid) {
-        hipLaunchKernelGGL((invalid_kernel<K, Idx>), dim3((unsigned)q.n), dim3(256), 0, st, p);
+        hipLaunchKernelGGL((invalid_kernel<K, Idx>), dim3((unsigned)std::min<int64_t>(q.n, kMaxGridX)), dim3(256), 0,
+                           st, p);
         he = hipGetLastError();
         if (he != hipSuccess) return (int)he;
     }

@@ -7,6 +7,10 @@ typedef struct ihipStream_t *hipStream_t;
 
 namespace kmc {
 typedef struct ihipEvent_t *hipEvent_t;
+// Grid extents of the per-record / per-list helper kernels, which loop over the
+// rest (a launch must keep gridDim * blockDim below 2^32 per dimension).
+constexpr int64_t kMaxGridX = 1 << 20;
+constexpr int64_t kMaxGridY = 32768;
 // kmc_trace_set_events: recorded around the histogram kernel (k <= 8) or the
 // whole radix pipeline (k > 8) of the next dense count calls on this thread.
 extern thread_local hipEvent_t t_trace_before, t_trace_after;

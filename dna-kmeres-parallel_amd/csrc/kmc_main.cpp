@@ -10,7 +10,8 @@
 //                                                                    (main.cu:287-300)
 //   step 2: n x minKmeres2 launches       -> kmc_pair_distances, one launch
 //                                               (--dropin: n x minKmeres2_hip) (main.cu:326-344)
-//   parallel_results.csv, "%f\n" per entry of the packed upper triangle (main.cu:351-358)
+//   parallel_results.csv, "%f\n" per entry of the packed upper triangle (main.cu:351-358),
+//   and sequential_results.csv, the CPU path's distances (main.cu:194-202)
 // and the step-1 / step-2 / total event timers the reference prints.  Extras:
 // a histogram dump (--counts, F3 of SURVEY.md §8(f)), k up to 13 (the reference
 // kernel is k = 3 only), multi-GPU counting over RCCL (--gpus), canonical k <= 31
@@ -58,7 +59,8 @@ void usage(FILE *f) {
             "                    nonl (importSeqsNoNL: records also end at '>' headers)\n"
             "  --max-seqs N      the reference's MAX_SEQS cap (default %d, which keeps %d records\n"
             "                    like the reference); 0 = unlimited\n"
-            "  --out DIR         directory of parallel_results.csv (default .)\n"
+            "  --out DIR         directory of parallel_results.csv and sequential_results.csv\n"
+            "                    (default .)\n"
             "  --counts FILE     write the histogram: one line per k-mer code, 'kmer<TAB>c_0 .. c_n-1'\n"
             "                    (bin order of permutation(): first base least significant)\n"
             "  --no-distances    step 1 only (no step 2, no CSV)\n"
@@ -315,7 +317,7 @@ int run(const Options &o) {
     }
 
     // step 2 (main.cu:326-344)
-    std::vector<float> mins;
+    std::vector<float> mins, seq;
     const uint64_t npairs = n * (n > 0 ? n - 1 : 0) / 2;
     if (o.distances && npairs > 0) {
         float *d_mins = nullptr;
@@ -340,11 +342,21 @@ int run(const Options &o) {
         }
         mins.resize(npairs);
         HIPCHK(hipMemcpy(mins.data(), d_mins, npairs * sizeof(float), hipMemcpyDeviceToHost));
+        if (o.dropin) {
+            // the CPU path's distances (exact integer sums) for sequential_results.csv
+            KMCCHK(kmc_pair_distances(d_sum, n, d_idx, n, k, d_mins, nullptr, 0, st));
+            seq.resize(npairs);
+            HIPCHK(hipMemcpy(seq.data(), d_mins, npairs * sizeof(float), hipMemcpyDeviceToHost));
+        }
         HIPCHK(hipFree(d_mins));
     }
     if (o.distances) {
-        const std::string path = o.out_dir + "/parallel_results.csv";
-        if (write_csv(path, mins)) return 1;
+        // the reference writes both files for diffing (main.cu:178, 194-202, 216, 351-358):
+        // sequential_results.csv holds sequentialKmerCount2's distances (exact integer
+        // sums, here kmc_pair_distances), parallel_results.csv the GPU path's (the
+        // same numbers, or minKmeres2's float sums with --dropin)
+        if (write_csv(o.out_dir + "/parallel_results.csv", mins)) return 1;
+        if (write_csv(o.out_dir + "/sequential_results.csv", o.dropin ? seq : mins)) return 1;
     }
     if (!o.counts_path.empty()) {
         if (hsum.empty() && nb * n > 0) {

@@ -10,6 +10,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "kmc.h"
@@ -43,6 +47,24 @@ extern "C" int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k,
 
 namespace {
 
+// Communicators of one device set, created on first use (ncclCommInitAll is a
+// collective setup of its own, far dearer than a 21 MB all-reduce) and kept until
+// kmc_multi_release().
+std::mutex g_comm_mu;
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
+int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) {
+        std::vector<ncclComm_t> c(devs.size());
+        if (ncclCommInitAll(c.data(), (int)devs.size(), devs.data()) != ncclSuccess) return KMC_ERR_RCCL;
+        it = g_comms.emplace(devs, std::move(c)).first;
+    }
+    out = it->second;
+    return KMC_OK;
+}
+
 struct DevBufs {
     int dev = 0;
     hipStream_t st = nullptr;
@@ -51,6 +73,9 @@ struct DevBufs {
     int32_t *sum = nullptr;
     int32_t *inv = nullptr;
     void *ws = nullptr;
+    char *pin[2] = {nullptr, nullptr};  // pinned staging of the host -> device copy
+    hipEvent_t done[2] = {nullptr, nullptr};
+    int rc = KMC_OK;
 };
 
 void release(std::vector<DevBufs> &b) {
@@ -62,8 +87,67 @@ void release(std::vector<DevBufs> &b) {
         (void)hipFree(d.sum);
         (void)hipFree(d.inv);
         (void)hipFree(d.ws);
+        for (int j = 0; j < 2; ++j) {
+            if (d.pin[j]) (void)hipHostFree(d.pin[j]);
+            if (d.done[j]) (void)hipEventDestroy(d.done[j]);
+        }
         if (d.st) (void)hipStreamDestroy(d.st);
     }
+}
+
+constexpr size_t kStage = (size_t)32 << 20;  // bytes per pinned staging buffer
+
+// Host thread of one device: allocate, stream the shard + halo through two pinned
+// buffers (the host copy into one overlaps the DMA out of the other), count.  One
+// thread per device, so every device loads at the same time.
+void load_and_count(DevBufs &d, const char *data, const int64_t *indices, uint64_t num_seqs, int k,
+                    const kmc_shard &sh, bool want_invalid, size_t sum_bytes) {
+    auto bad = [&](int code) { d.rc = code; };
+    if (hipSetDevice(d.dev) != hipSuccess) return bad(KMC_ERR_NO_DEVICE);
+    if (hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking) != hipSuccess) return bad(KMC_ERR_NO_DEVICE);
+    // the device holds [base, read_hi) with base = read_lo rounded down to 16 so that
+    // the library's data pointer (device base - base) stays 16-byte aligned
+    const uint64_t base = sh.read_lo & ~(uint64_t)15;
+    const uint64_t len = sh.read_hi - base;
+    if (hipMalloc(&d.data, len + 16) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    if (hipMalloc(&d.idx, (num_seqs + 1) * sizeof(int64_t)) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    if (hipMalloc(&d.sum, sum_bytes) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    if (want_invalid && hipMalloc(&d.inv, num_seqs * sizeof(int32_t)) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    for (int j = 0; j < 2; ++j) {
+        if (hipHostMalloc(reinterpret_cast<void **>(&d.pin[j]), kStage, hipHostMallocDefault) != hipSuccess)
+            return bad(KMC_ERR_NOMEM);
+        if (hipEventCreateWithFlags(&d.done[j], hipEventDisableTiming) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    }
+    kmc_dense_args a{};
+    a.data = d.data - base;
+    a.indices = d.idx;
+    a.num_seqs = num_seqs;
+    a.k = k;
+    a.sum = d.sum;
+    a.sum_ld = num_seqs;
+    a.invalid = d.inv;
+    a.read_lo = sh.read_lo;
+    a.read_hi = sh.read_hi;
+    a.win_lo = sh.win_lo;
+    a.win_hi = sh.win_hi;
+    const size_t wsb = kmc_count_dense_ex_workspace_size(&a, d.dev);
+    if (wsb == 0 || hipMalloc(&d.ws, wsb) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    a.workspace = d.ws;
+    a.workspace_bytes = wsb;
+    // indices are small: one synchronous copy
+    if (hipMemcpy(d.idx, indices, (num_seqs + 1) * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
+        return bad(KMC_ERR_NOMEM);
+    uint64_t done = 0;
+    for (int j = 0; done < len; j ^= 1) {
+        const size_t c = (size_t)std::min<uint64_t>(kStage, len - done);
+        if (hipEventSynchronize(d.done[j]) != hipSuccess) return bad(KMC_ERR_NOMEM);  // buffer j free again
+        std::memcpy(d.pin[j], data + base + done, c);
+        if (hipMemcpyAsync(d.data + done, d.pin[j], c, hipMemcpyHostToDevice, d.st) != hipSuccess ||
+            hipEventRecord(d.done[j], d.st) != hipSuccess)
+            return bad(KMC_ERR_NOMEM);
+        done += c;
+    }
+    d.rc = kmc_count_dense_ex(&a, d.st);
 }
 
 }  // namespace
@@ -80,6 +164,8 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     for (int i = 0; i < ndev; ++i) {
         devs[i] = devices ? devices[i] : i;
         if (devs[i] < 0 || devs[i] >= visible) return KMC_ERR_INVALID_ARG;
+        for (int j = 0; j < i; ++j)
+            if (devs[j] == devs[i]) return KMC_ERR_INVALID_ARG;  // one communicator rank per device
     }
     std::vector<kmc_shard> sh(ndev);
     int rc = kmc_plan_shards(indices, num_seqs, k, ndev, 4096, sh.data());
@@ -95,45 +181,22 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
         (void)hipSetDevice(cur);
         return code;
     };
-    for (int i = 0; i < ndev; ++i) {
-        DevBufs &d = b[i];
-        d.dev = devs[i];
-        if (hipSetDevice(d.dev) != hipSuccess) return fail(KMC_ERR_NO_DEVICE);
-        if (hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking) != hipSuccess) return fail(KMC_ERR_NO_DEVICE);
-        // the device holds [base, read_hi) with base = read_lo rounded down to 16 so that
-        // the library's data pointer (device base - base) stays 16-byte aligned
-        const uint64_t base = sh[i].read_lo & ~(uint64_t)15;
-        const uint64_t len = sh[i].read_hi - base;
-        if (hipMalloc(&d.data, len + 16) != hipSuccess) return fail(KMC_ERR_NOMEM);
-        if (hipMalloc(&d.idx, (num_seqs + 1) * sizeof(int64_t)) != hipSuccess) return fail(KMC_ERR_NOMEM);
-        if (hipMalloc(&d.sum, sum_bytes) != hipSuccess) return fail(KMC_ERR_NOMEM);
-        if (invalid && hipMalloc(&d.inv, num_seqs * sizeof(int32_t)) != hipSuccess) return fail(KMC_ERR_NOMEM);
-        kmc_dense_args a{};
-        a.data = d.data - base;
-        a.indices = d.idx;
-        a.num_seqs = num_seqs;
-        a.k = k;
-        a.sum = d.sum;
-        a.sum_ld = num_seqs;
-        a.invalid = d.inv;
-        a.read_lo = sh[i].read_lo;
-        a.read_hi = sh[i].read_hi;
-        a.win_lo = sh[i].win_lo;
-        a.win_hi = sh[i].win_hi;
-        const size_t wsb = kmc_count_dense_ex_workspace_size(&a, d.dev);
-        if (wsb == 0 || hipMalloc(&d.ws, wsb) != hipSuccess) return fail(KMC_ERR_NOMEM);
-        a.workspace = d.ws;
-        a.workspace_bytes = wsb;
-        if (hipMemcpyAsync(d.data, data + base, len, hipMemcpyHostToDevice, d.st) != hipSuccess ||
-            hipMemcpyAsync(d.idx, indices, (num_seqs + 1) * sizeof(int64_t), hipMemcpyHostToDevice, d.st) !=
-                hipSuccess)
-            return fail(KMC_ERR_NOMEM);
-        rc = kmc_count_dense_ex(&a, d.st);
-        if (rc) return fail(rc);
+    {
+        std::vector<std::thread> th;
+        th.reserve(ndev);
+        for (int i = 0; i < ndev; ++i) {
+            b[i].dev = devs[i];
+            th.emplace_back(load_and_count, std::ref(b[i]), data, indices, num_seqs, k, std::cref(sh[i]),
+                            invalid != nullptr, sum_bytes);
+        }
+        for (auto &t : th) t.join();
     }
+    for (auto &d : b)
+        if (d.rc) return fail(d.rc);
     // one all-reduce of the int32 matrix (and the invalid vector) over xGMI
-    std::vector<ncclComm_t> comms(ndev);
-    if (ncclCommInitAll(comms.data(), ndev, devs.data()) != ncclSuccess) return fail(KMC_ERR_RCCL);
+    std::vector<ncclComm_t> comms;
+    rc = comms_for(devs, comms);
+    if (rc) return fail(rc);
     ncclResult_t nr = ncclGroupStart();
     for (int i = 0; i < ndev && nr == ncclSuccess; ++i) {
         nr = ncclAllReduce(b[i].sum, b[i].sum, nb * num_seqs, ncclInt32, ncclSum, comms[i], b[i].st);
@@ -150,8 +213,15 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
             nr = ncclSystemError;
         if (hipStreamSynchronize(b[0].st) != hipSuccess) nr = ncclSystemError;
     }
-    for (auto &c : comms) ncclCommDestroy(c);
     release(b);
     (void)hipSetDevice(cur);
     return nr == ncclSuccess ? KMC_OK : KMC_ERR_RCCL;
+}
+
+extern "C" int kmc_multi_release(void) {
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    for (auto &e : g_comms)
+        for (auto &c : e.second) ncclCommDestroy(c);
+    g_comms.clear();
+    return KMC_OK;
 }

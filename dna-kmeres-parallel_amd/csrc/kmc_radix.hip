@@ -20,6 +20,7 @@
 // as the k <= 8 kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <mutex>
 #include <vector>
@@ -369,37 +370,40 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
     constexpr int kWords = LOW <= 15 ? kBucketBins : kBucketBins / 2;
     __shared__ __attribute__((aligned(16))) uint32_t h[kWords];
     __shared__ unsigned long long s_sum;
-    const int64_t list = blockIdx.x;  // s*nbk + b
-    const int64_t s = list / p.nbk, b = list % p.nbk;
-    for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
-    if (threadIdx.x == 0) s_sum = 0ull;
-    __syncthreads();
-    const uint64_t beg = p.off[list * p.G], end = p.off[(list + 1) * p.G];
-    hist_list<LOW, false>(p.ent, beg, end, h, 0u);
-    __syncthreads();
-    uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
-    if constexpr (LOW <= 15) {
-        for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
-    } else {
-        uint32_t part = 0u;
-        for (int i = threadIdx.x; i < kWords; i += 1024) part += (h[i] & 0xFFFFu) + (h[i] >> 16);
-        atomicAdd(&s_sum, (unsigned long long)part);
+    const int64_t nlists = p.n * p.nbk;
+    for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
+        const int64_t s = list / p.nbk, b = list % p.nbk;
+        for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+        if (threadIdx.x == 0) s_sum = 0ull;
         __syncthreads();
-        if (s_sum == end - beg) {
-            for (int i = threadIdx.x; i < kWords; i += 1024) {
-                const uint32_t w = h[i];
-                reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
-            }
-        } else {  // a bin wrapped: exact recount, half of the bins at a time
-            for (uint32_t half = 0; half < 2; ++half) {
-                __syncthreads();
-                for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
-                __syncthreads();
-                hist_list<LOW, true>(p.ent, beg, end, h, half);
-                __syncthreads();
-                for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
+        const uint64_t beg = p.off[list * p.G], end = p.off[(list + 1) * p.G];
+        hist_list<LOW, false>(p.ent, beg, end, h, 0u);
+        __syncthreads();
+        uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
+        if constexpr (LOW <= 15) {
+            for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
+        } else {
+            uint32_t part = 0u;
+            for (int i = threadIdx.x; i < kWords; i += 1024) part += (h[i] & 0xFFFFu) + (h[i] >> 16);
+            atomicAdd(&s_sum, (unsigned long long)part);
+            __syncthreads();
+            if (s_sum == end - beg) {
+                for (int i = threadIdx.x; i < kWords; i += 1024) {
+                    const uint32_t w = h[i];
+                    reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
+                }
+            } else {  // a bin wrapped: exact recount, half of the bins at a time
+                for (uint32_t half = 0; half < 2; ++half) {
+                    __syncthreads();
+                    for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+                    __syncthreads();
+                    hist_list<LOW, true>(p.ent, beg, end, h, half);
+                    __syncthreads();
+                    for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
+                }
             }
         }
+        __syncthreads();  // h and s_sum are reused by the next list
     }
 }
 
@@ -413,26 +417,29 @@ __global__ __launch_bounds__(256) void radix_place_kernel(RParams p, int64_t nbi
     }
 }
 
-// invalid[s] = windows in range - sum of the record's bucket counts
+// invalid[s] = windows in range - sum of the record's bucket counts; records
+// blockIdx.x, blockIdx.x + gridDim.x, ...
 template <int K, class Idx>
 __global__ __launch_bounds__(256) void radix_invalid_kernel(RParams p) {
-    const int64_t s = blockIdx.x;
     const int64_t m = (int64_t)p.nbk * p.G;
-    uint64_t acc = 0;
-    for (int64_t i = threadIdx.x; i < m; i += 256) acc += p.cnt[s * m + i];
     __shared__ uint64_t red[256];
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    for (int64_t s = blockIdx.x; s < p.n; s += gridDim.x) {
+        uint64_t acc = 0;
+        for (int64_t i = threadIdx.x; i < m; i += 256) acc += p.cnt[s * m + i];
+        red[threadIdx.x] = acc;
         __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const Geom g = make_geom<Idx>(p);
-        int64_t ca, ce;
-        record_windows<K, Idx>(p, g, s, ca, ce);
-        const int64_t nw = ce > ca ? ce - ca : 0;
-        p.invalid[s] = (int32_t)(nw - (int64_t)red[0]);
+        for (int st = 128; st > 0; st >>= 1) {
+            if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            const Geom g = make_geom<Idx>(p);
+            int64_t ca, ce;
+            record_windows<K, Idx>(p, g, s, ca, ce);
+            const int64_t nw = ce > ca ? ce - ca : 0;
+            p.invalid[s] = (int32_t)(nw - (int64_t)red[0]);
+        }
+        __syncthreads();
     }
 }
 
@@ -474,16 +481,18 @@ inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap) {
 }
 
 std::mutex r_mu;
-int r_cus = 0, r_occ = 0;
+std::vector<int> r_cus;  // CUs per device
 
 int r_grid(int device, int &G) {
     std::lock_guard<std::mutex> lk(r_mu);
-    if (r_cus == 0) {
-        hipError_t e = hipDeviceGetAttribute(&r_cus, hipDeviceAttributeMultiprocessorCount, device);
+    if ((int)r_cus.size() <= device) r_cus.resize(device + 1, 0);
+    if (r_cus[device] == 0) {
+        int v = 0;
+        hipError_t e = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device);
         if (e != hipSuccess) return (int)e;
-        r_occ = 1;  // one 16-wave workgroup per CU: fewer open lists than more, smaller groups
+        r_cus[device] = v;
     }
-    G = r_cus * r_occ;
+    G = r_cus[device];  // one 16-wave workgroup per CU: fewer open lists than more, smaller groups
     return 0;
 }
 
@@ -570,14 +579,16 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
         p.b_hi = p.b_lo + p.nbk / groups;
         hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, true, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
     }
-    hipLaunchKernelGGL((radix_hist_kernel<low_bits(K)>), dim3((unsigned)(n * p.nbk)), dim3(1024), 0, st, p, nbins);
+    hipLaunchKernelGGL((radix_hist_kernel<low_bits(K)>), dim3((unsigned)std::min<int64_t>(n * p.nbk, kMaxGridX)),
+                       dim3(1024), 0, st, p, nbins);
     hipLaunchKernelGGL(radix_place_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st, p, nbins);
     if (t_trace_after) {
         he = hipEventRecord(t_trace_after, st);
         if (he != hipSuccess) return (int)he;
     }
     if (a->invalid)
-        hipLaunchKernelGGL((radix_invalid_kernel<K, int64_t>), dim3((unsigned)n), dim3(256), 0, st, p);
+        hipLaunchKernelGGL((radix_invalid_kernel<K, int64_t>), dim3((unsigned)std::min<int64_t>(n, kMaxGridX)),
+                           dim3(256), 0, st, p);
     he = hipGetLastError();
     return (int)he;
 }

@@ -74,6 +74,7 @@ def lib():
         L.kmc_trace_set_events.argtypes = [_P, _P]
         L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
         L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
+        L.kmc_multi_release.argtypes = []
         L.kmc_synth_fill.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
         L.kmc_synth_fill_range.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
         L.kmc_synth_indices.argtypes = [_P, _U64, _U64]

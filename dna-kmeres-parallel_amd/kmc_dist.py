@@ -17,21 +17,27 @@ import kmc
 
 def gpu_counter(device):
     """Partial histogram of one shard on `device` with the HIP kernel: only the
-    shard's bytes plus its halo are copied to the device."""
+    shard's bytes plus its halo are copied to the device.  The library picks its
+    workspace and CU count from the current HIP device, so the call runs with
+    `device` current and on that device's stream, whatever the caller's current
+    device is."""
     import torch
+
+    device = torch.device(device)
 
     def count(data, indices, k, shard):
         win_lo, win_hi, read_lo, read_hi = shard
         n = len(indices) - 1
-        out = torch.zeros((1 << (2 * k), n), dtype=torch.int32, device=device)
-        if win_hi <= win_lo:
-            return out
-        base = read_lo & ~15  # keep (device pointer - base) 16-byte aligned
-        chunk = torch.from_numpy(np.ascontiguousarray(data[base:read_hi])).to(device)
-        idx = torch.from_numpy(np.ascontiguousarray(indices, dtype=np.int64)).to(device)
-        args = kmc.dense_args(chunk, idx, k, out, read=(read_lo, read_hi), win=(win_lo, win_hi),
-                              data_offset=base)
-        kmc.count_dense_ex(args)
+        with torch.cuda.device(device):
+            out = torch.zeros((1 << (2 * k), n), dtype=torch.int32, device=device)
+            if win_hi <= win_lo:
+                return out
+            base = read_lo & ~15  # keep (device pointer - base) 16-byte aligned
+            chunk = torch.from_numpy(np.ascontiguousarray(data[base:read_hi])).to(device)
+            idx = torch.from_numpy(np.ascontiguousarray(indices, dtype=np.int64)).to(device)
+            args = kmc.dense_args(chunk, idx, k, out, read=(read_lo, read_hi), win=(win_lo, win_hi),
+                                  data_offset=base)
+            kmc.count_dense_ex(args, stream=torch.cuda.current_stream(device))
         return out
 
     return count

@@ -90,7 +90,11 @@ int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_
  *   sum         device int32[4^k * num_seqs], overwritten (layout above)
  *   invalid     optional device int32[num_seqs]: invalid windows (CPU bin 0)
  *   workspace   device scratch of kmc_count_dense_workspace_size() bytes, or
- *               NULL to use a library-owned buffer (not graph-capture safe).  */
+ *               NULL to use a library-owned buffer, one per device, shared by
+ *               every NULL-workspace call on that device: such calls must not
+ *               overlap (one stream, or the caller serialises them), and they are
+ *               not graph-capture safe.  Concurrent calls pass their own workspace.
+ * The same holds for the NULL workspace of kmc_pair_distances.  */
 size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device);
 
 int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,
@@ -138,9 +142,14 @@ int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, int nshard
  * halo to its device, counts it there (kmc_count_dense_ex) and sums the per-device
  * matrices with one RCCL all-reduce (int32, sum) over xGMI; the result
  * sum[s + num_seqs*code] (and optional invalid[s]) is copied back to host
- * memory.  devices == NULL -> 0 .. ndev-1.  Synchronous. */
+ * memory.  devices == NULL -> 0 .. ndev-1 (distinct devices).  Synchronous.
+ * One host thread per device streams its shard through pinned staging buffers,
+ * so all devices load concurrently.  The RCCL communicators of a device set are
+ * created on its first call and reused until kmc_multi_release(). */
 int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes, int k,
                     int ndev, const int *devices, int32_t *sum, int32_t *invalid);
+/* Destroys the communicators cached by kmc_count_multi. */
+int kmc_multi_release(void);
 
 /* ------------------------------------------------------------------------ */
 /* Pairwise k-mer distance (the reference's step 2).

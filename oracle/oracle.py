@@ -37,7 +37,7 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        path = os.path.join(HERE, "libkmc_oracle.so")
+        path = os.environ.get("KMC_ORACLE_LIB") or os.path.join(HERE, "libkmc_oracle.so")
         if not os.path.exists(path):
             build(ref=False)
         L = ctypes.CDLL(path)

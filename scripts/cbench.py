@@ -118,6 +118,81 @@ def c4_cpu_baseline(data, idx, k, sample):
                       % (th, sample, dt, cpu_model())}
 
 
+def check_c3(torch, kmc, data, idx, out, recs, L, k, slice_bases=4_000_000):
+    """Parity of the timed C3 call: every record's column sums to its L - k + 1
+    windows (uniform ACGT, no invalid window), and a 4 Mbase window range of
+    record 3 counted through the same radix path equals the oracle's histogram of
+    that range."""
+    import numpy as np
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    import oracle
+    col = torch.zeros(recs, dtype=torch.int64, device=out.device)
+    for c0 in range(0, out.shape[0], 1 << 22):
+        col += out[c0:c0 + (1 << 22)].to(torch.int64).sum(dim=0)
+    sums = col.cpu().numpy()
+    assert (sums == L - k + 1).all(), "C3 column sums %s != %d" % (sums, L - k + 1)
+    r = 3 % recs
+    lo = r * (L + 1) + 123_457
+    hi = lo + slice_bases
+    part = torch.zeros_like(out)
+    kmc.count_dense_ex(kmc.dense_args(data, idx, k, part, read=(lo, hi + k - 1), win=(lo, hi)))
+    torch.cuda.synchronize()
+    host = data[lo:hi + k - 1].cpu().numpy()
+    exp, _ = oracle.count_dense(np.append(host, np.uint8(0)), np.array([0, host.size + 1], np.int64), k)
+    got = part[:, r].cpu().numpy()
+    assert (got == exp[:, 0]).all(), "C3 slice histogram differs from the oracle"
+    assert int(part.to(torch.int64).sum()) == slice_bases
+    return {"column_sums": "all %d == L-k+1" % recs, "slice": "record %d windows [%d, %d) == oracle" % (r, lo, hi)}
+
+
+def check_c4(torch, kmc, data, idx, k, keys, counts, off, slice_bases=2_000_000):
+    """Parity of the timed C4 call: the counts sum to the valid (soft-masked ACGT)
+    windows, counted independently on the device, every key is <= its reverse
+    complement, and a 2 Mbase slice counted as its own record equals the oracle."""
+    import numpy as np
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "oracle"))
+    import oracle
+    lut = torch.zeros(256, dtype=torch.int32, device=data.device)
+    for ch in b"ACGTacgt":
+        lut[ch] = 1
+    valid = 0
+    step = 1 << 28
+    n = data.numel()
+    for o in range(0, n, step):
+        e = min(n, o + step + k - 1)
+        v = lut[data[o:e].long()]
+        cs = torch.cumsum(torch.nn.functional.pad(v, (1, 0)), 0)
+        w = cs[k:] - cs[:-k]  # bases o + i .. o + i + k - 1
+        m = min(step, n - o)
+        valid += int((w[:m] == k).sum())
+    tot = int(counts.to(torch.int64).sum())
+    assert tot == valid, "C4 counts sum %d != valid windows %d" % (tot, valid)
+    mask = (1 << (2 * k)) - 1
+    kk = keys[:: max(1, keys.numel() // 100_000)].cpu().numpy().astype(np.uint64)
+    rc = np.zeros_like(kk)
+    x = kk.copy()
+    for _ in range(k):
+        rc = (rc << np.uint64(2)) | (np.uint64(3) - (x & np.uint64(3)))
+        x >>= np.uint64(2)
+    assert (kk <= rc).all() and (kk <= np.uint64(mask)).all(), "C4 key above its reverse complement"
+    lo = int(idx[1].item()) + 5_000_000
+    sl = data[lo:lo + slice_bases]
+    buf = torch.zeros(slice_bases + 16, dtype=torch.uint8, device=data.device)
+    buf[:slice_bases] = sl
+    sidx = torch.tensor([0, slice_bases + 1], dtype=torch.int64, device=data.device)
+    gk, gc, _ = kmc.count_canonical(buf, sidx, k, flags=kmc.CANON_SOFTMASK)
+    host = np.append(sl.cpu().numpy(), np.uint8(0))
+    ek, ec, _ = oracle.count_canonical(host, np.array([0, host.size], np.int64), k, soft=True)
+    got = dict(zip(gk.cpu().numpy().astype(np.uint64).tolist(), gc.cpu().numpy().tolist()))
+    exp = dict(zip(ek.astype(np.uint64).tolist(), ec.tolist()))
+    assert got == exp, "C4 slice differs from the oracle"
+    return {"sum_counts": "== %d valid windows (independent device count)" % valid,
+            "keys_canonical": "sampled keys <= reverse complement",
+            "slice": "record 1 bases [%d, %d) as a record == oracle (%d distinct)" % (lo, lo + slice_bases, len(exp))}
+
+
 def timed(torch, fn, iters):
     fn()
     torch.cuda.synchronize()
@@ -141,6 +216,7 @@ def main():
     ap.add_argument("--k3", type=int, default=13)
     ap.add_argument("--cpu-sample-c3", type=int, default=2_000_000, help="bases per CPU thread (0 = skip)")
     ap.add_argument("--cpu-sample-c4", type=int, default=16_000_000, help="bases per CPU thread (0 = skip)")
+    ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity checks")
     a = ap.parse_args()
     import torch
     import kmc
@@ -162,6 +238,8 @@ def main():
         alg = data.numel() + 4 * (1 << (2 * k)) * recs
         line = {"config": "C3", "k": k, "records": recs, "bases": recs * L, "s_med": med, "s_min": best,
                 "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9, "frac8TB": alg / med / 8e12}
+        if a.check:
+            line["parity"] = check_c3(torch, kmc, data, idx, out, recs, L, k)
         if a.cpu_sample_c3 > 0:
             line["cpu_baseline"] = c3_cpu_baseline(data, L, k, a.cpu_sample_c3)
         print(json.dumps(line), flush=True)
@@ -183,6 +261,8 @@ def main():
         line = {"config": "C4", "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
                 "valid_windows": tot, "distinct": int(keys.numel()), "s_med": med, "s_min": best,
                 "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9, "frac8TB": alg / med / 8e12}
+        if a.check:
+            line["parity"] = check_c4(torch, kmc, data, idx, k, keys, counts, off)
         if a.cpu_sample_c4 > 0:
             line["cpu_baseline"] = c4_cpu_baseline(data, idx, k, a.cpu_sample_c4)
         print(json.dumps(line), flush=True)

@@ -112,7 +112,7 @@ def make_cases():
 
 
 KS_ALL = (1, 2, 3, 4, 5)
-KS_BIG = {"basic": (8,), "random": (8, 11), "crlf": (8,)}
+KS_BIG = {"basic": (8, 13), "random": (8, 11, 12, 13), "crlf": (8,)}
 
 
 def main():

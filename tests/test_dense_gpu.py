@@ -401,3 +401,38 @@ def test_bench_rank_counts_sum_to_whole(kmc, oracle, cuda, scaling, world, recor
     total = int(p["indices"][-1])
     exp, _ = oracle.count_dense(kmc.synth_host_range(0, total, L, seed), p["indices"], k)
     np.testing.assert_array_equal(acc, exp)
+
+
+@pytest.mark.parametrize("k,n", [(8, 70_000), (9, 65_600)])
+def test_many_short_records(kmc, oracle, cuda, k, n):
+    """More records than one grid dimension of the per-record helper kernels can
+    hold (k = 8: reduce/invalid; k = 9: the per-list histogram, n * 64 lists of
+    1024 threads > 2^32): output 18 GB / 69 GB, checked on the device (every
+    column sums to the record's valid windows) and on a sample of records against
+    the oracle.  A caller workspace keeps the library's cache small afterwards."""
+    import torch
+    rng = np.random.default_rng(600 + k)
+    lens = rng.integers(0, 3 * k, size=n)
+    lens[:: 997] = 5000  # a few records cut across workgroups
+    data, idx = random_records(rng, lens, 0.01, 0.0)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    out = torch.empty((1 << (2 * k), n), dtype=torch.int32, device=cuda)
+    inv = torch.empty(n, dtype=torch.int32, device=cuda)
+    args = kmc.dense_args(d, di, k, out, invalid=inv)
+    ws = torch.empty(kmc.dense_ex_workspace_size(args), dtype=torch.uint8, device=cuda)
+    kmc.count_dense_ex(kmc.dense_args(d, di, k, out, invalid=inv, workspace=ws))
+    torch.cuda.synchronize()
+    del ws
+    col = torch.zeros(n, dtype=torch.int64, device=cuda)
+    for c0 in range(0, 1 << (2 * k), 4096):
+        col += out[c0:c0 + 4096].to(torch.int64).sum(dim=0)
+    windows = np.maximum(lens - k + 1, 0)
+    np.testing.assert_array_equal(col.cpu().numpy() + inv.cpu().numpy(), windows)
+    sample = np.unique(np.concatenate([rng.integers(0, n, 40), np.arange(0, n, 997)[:20], [0, n - 1]]))
+    for s in sample:
+        seg = data[idx[s]:idx[s + 1]]
+        exp, exp_inv = oracle.count_dense(seg, np.array([0, seg.size], np.int64), k)
+        np.testing.assert_array_equal(out[:, s].cpu().numpy(), exp[:, 0], err_msg="record %d" % s)
+        assert int(inv[s]) == int(exp_inv[0])
+    del out
+    torch.cuda.empty_cache()

@@ -66,6 +66,43 @@ def test_oracle_matches_reference_live(oracle, k):
         np.testing.assert_array_equal(got[:, s], h[1:])
 
 
+_K13_LIVE = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import oracle
+rng = np.random.default_rng(113)
+recs = []
+for L in (0, 12, 13, 14, 40_000, 2_500):
+    x = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=L)
+    x[rng.random(L) < 0.003] = ord("N")
+    recs.append(np.append(x, np.uint8(0)))
+data = np.concatenate(recs)
+idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+got, inv = oracle.count_dense(data, idx, 13)
+bad = 0
+for s in range(idx.size - 1):
+    h = oracle.ref_count_bytes(data[idx[s]:idx[s + 1]], 13)
+    bad += int(h[0] != inv[s]) + int((got[:, s] != h[1:]).sum())
+print("mismatches", bad, flush=True)
+os._exit(0 if bad == 0 else 1)  # skip the 4^13-entry std::map's destructor (tens of seconds)
+"""
+
+
+def test_oracle_matches_reference_live_k13(oracle):
+    """k = 13 (config C3, the largest dense k) against the reference's own
+    permutationsCountAll, whose 4^13-entry std::map is built and dropped in a
+    child process."""
+    import subprocess
+    import sys
+    if not oracle.have_ref_cpu():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    r = subprocess.run([sys.executable, "-c", _K13_LIVE, os.path.dirname(oracle.__file__)], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout
+
+
 def test_oracle_range_partition_sums(oracle):
     """Windowed counting over disjoint start ranges sums to the full count."""
     rng = np.random.default_rng(7)
