@@ -5,19 +5,20 @@
 // kernels.h:142), computed by a two-level radix partition:
 //
 //   R1 count    every workgroup streams its tiles (kmc_stream.h) and counts, per
-//               record piece, the windows of each bucket b = code >> 15 in LDS
+//               record piece, the windows of each bucket b = code >> LOW in LDS
 //               -> cnt[(s*NBK + b)*G + w]
 //   R2 scan     exclusive prefix sum -> 64-bit offsets: list (s, b) is contiguous,
 //               workgroup segments inside it in w order
-//   R3 scatter  the same traversal writes each window's low 15 code bits
-//               (uint16) at its list position (LDS 64-bit cursors per bucket)
-//   R4 hist     one workgroup per list: 32 768-bin LDS histogram of its entries ->
-//               stage[s][b*32768 + c] (record-major, coalesced)
+//   R3 scatter  the same traversal appends each window's low LOW code bits
+//               (uint16) to its bucket's LDS ring and writes complete 64-byte
+//               list segments (radix_ring_kernel)
+//   R4 hist     one workgroup per list: 2^LOW-bin LDS histogram of its entries ->
+//               stage[s][b*2^LOW + c] (record-major, coalesced)
 //   R5 place    transpose stage into sum[s + ld*code] (k-mer-major, coalesced)
 //
-// Bytes per k-mer: 1 (R1) + 1 (R3) input, 2 written + 2 read entries, plus the
-// output twice; the LDS histograms see the same bank-conflict-bound atomic rate
-// as the k <= 8 kernels.
+// LOW = min(2k - 6, 15), 16 from k = 12 on (low_bits).  Bytes per k-mer: 1 (R1) +
+// 1 (R3) input, 2 written + 2 read entries, plus the output twice; the LDS
+// histograms see the same bank-conflict-bound atomic rate as the k <= 8 kernels.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,24 +31,9 @@
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
-// Diagnostic builds only (scripts/kbench.py timing): 1 = no list stores, 2 = also
-// non-returning bucket counts, 3 = staging without the flush.  Results are wrong.
-#ifndef KMC_RSCAT_ABL
-#define KMC_RSCAT_ABL 0
-#endif
-// tile prefetch depth of the scatter pass (register pressure: the round's windows
-// stay in registers across the barrier)
+// tile prefetch depth of the scatter pass
 #ifndef KMC_RSCAT_PF
 #define KMC_RSCAT_PF 2
-#endif
-// tiles per wave in one R3 round (the round is counting-sorted in LDS: 64 KB of
-// staging per tile and wave group)
-#ifndef KMC_RSCAT_RT
-#define KMC_RSCAT_RT 2
-#endif
-// write-out loop unroll (entries in flight per lane; register pressure)
-#ifndef KMC_RSCAT_WU
-#define KMC_RSCAT_WU 16
 #endif
 
 namespace kmc {
@@ -74,7 +60,6 @@ struct RParams {
     int derive;
     int G;           // workgroups of R1/R3
     int nbk;         // buckets per record
-    int b_lo, b_hi;  // R3: buckets scattered by this launch
     uint32_t *cnt;   // [n][nbk][G]
     uint64_t *off;   // [n*nbk*G + 1] exclusive prefix of cnt
     uint16_t *ent;   // entries
@@ -101,166 +86,15 @@ struct RCountOp {
     __device__ void after_iter(int64_t, int64_t, bool) {}
 };
 
-// R3 op.  Scattering every window straight to its list costs one L2 write
-// request per 2-byte entry (64 per wave store); instead each round of RT tiles
-// per wave is counting-sorted by bucket in LDS and written out so that
-// consecutive lanes store consecutive entries of one list.  A window's rank in
-// its bucket is taken (returning LDS add) as the tile is decoded; the lane keeps
-// only the tile's bases (lo, hi, valid mask) and the ranks, and recomputes the
-// codes once the round's scan has placed the buckets.
-//   srt  [NW*1024*RT] the round sorted by bucket
-//   off  [NBK + 1]    bucket counts -> exclusive offsets within srt
-//   gcur [NBK]        global position of each list's next entry (this workgroup)
-//   gdel [NBK]        this round: global position of srt index 0 of each bucket's run
-// Only buckets [b_lo, b_lo + b_n) are scattered (bucket-group launches).
-template <int K, int NW, int RT>
-struct RStageOp {
-    static constexpr int LOW = low_bits(K);
-    static constexpr int NBK = 1 << (2 * K - LOW);
-    static constexpr int BATCH = NW * 1024 * RT;
-    static_assert(BATCH <= 65536, "ranks are 16-bit");
-    static constexpr uint32_t kNone = 0xFFFFFFFFu;
-    uint32_t *srt, *off, *nw;
-    unsigned long long *gcur;
-    long long *gdel;
-    uint16_t *ent;
-    uint32_t b_lo, b_n;
-    int wave, lane, tid;
-    int slot;              // tiles of this round held (workgroup-uniform)
-    uint32_t lo[RT], hi[RT], wm[RT];  // per held tile: bases and windows taken (0: none)
-    uint32_t rank[RT][8];  // their ranks in their buckets, two 16-bit ranks per word (< BATCH)
-
-    __device__ void before_tile() {}
-
-    __device__ __forceinline__ bool take(uint32_t c, uint32_t W, int j) const {
-        return ((W >> j) & 1u) && ((c >> LOW) - b_lo) < b_n;
-    }
-
-    template <int S>
-    __device__ __forceinline__ void rank_tile(uint32_t l, uint32_t h, uint32_t W) {
-        lo[S] = l;
-        hi[S] = h;
-        uint32_t m = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t c = window_code_rt<K>(l, h, j);
-            const bool v = take(c, W, j);
-            uint32_t r = 0;
-            if (v) r = __hip_atomic_fetch_add(&off[(c >> LOW) - b_lo], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            m |= (uint32_t)v << j;
-            if (j & 1) rank[S][j >> 1] |= r << 16;
-            else rank[S][j >> 1] = r;
-        }
-        wm[S] = m;
-    }
-
-    template <bool MASKED>
-    __device__ __forceinline__ void tile(uint32_t l, uint32_t h, uint32_t W) {
-        if constexpr (RT == 1) {
-            rank_tile<0>(l, h, W);
-        } else {
-            static_assert(RT == 2, "one or two tiles per round");
-            if (slot == 0) rank_tile<0>(l, h, W);
-            else rank_tile<1>(l, h, W);
-        }
-    }
-
-    __device__ void after_iter(int64_t i, int64_t per, bool) {
-        if (++slot < RT && i + 1 < per) return;  // round not full (i, per, slot: workgroup-uniform)
-        slot = 0;
-        lds_barrier();  // every rank taken
-#if KMC_RSCAT_ABL == 3
-#pragma unroll
-        for (int S = 0; S < RT; ++S) wm[S] = 0u;
-        lds_barrier();
-        return;  // diagnostic: ranking only
-#endif
-        // exclusive scan of the bucket counts (off[b_n] = round total)
-        block_scan_inplace(off, (int)b_n);
-        // counting-sort the round into srt; per bucket, the global position of srt
-        // index 0 (gdel = cursor - offset) and the advanced cursor
-#pragma unroll
-        for (int S = 0; S < RT; ++S) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t c = window_code_rt<K>(lo[S], hi[S], j);
-                if ((wm[S] >> j) & 1u)
-                    srt[off[(c >> LOW) - b_lo] + ((rank[S][j >> 1] >> (16 * (j & 1))) & 0xFFFFu)] = c;
-            }
-            wm[S] = 0u;
-        }
-        for (uint32_t b = tid; b < b_n; b += NW * 64) {
-            const uint32_t o0 = off[b], o1 = off[b + 1];
-            const unsigned long long g = gcur[b];
-            gdel[b] = (long long)g - (long long)o0;
-            gcur[b] = g + (o1 - o0);
-        }
-        const uint32_t total = off[b_n];
-        lds_barrier();
-        // coalesced write-out: srt[i] is entry i + gdel[b] of bucket b's list; the
-        // counts are cleared for the next round (nothing reads them until then)
-        for (uint32_t b = tid; b <= b_n; b += NW * 64) off[b] = 0u;
-#pragma unroll KMC_RSCAT_WU
-        for (int q = 0; q < 16 * RT; ++q) {
-            const uint32_t i = tid + q * NW * 64;
-            if (i >= total) break;
-            const uint32_t c = srt[i];
-            const long long pos = gdel[(c >> LOW) - b_lo] + (long long)i;
-#if KMC_RSCAT_ABL >= 1
-            if (c == 0xFFFFFFFEu)  // diagnostic: never true, keeps the loads
-#endif
-            ent[pos] = (uint16_t)(c & ((1u << LOW) - 1));
-        }
-        lds_barrier();  // srt and the counts are free for the next round
-    }
-
-    // in-place exclusive scan of a[0..m) with a[m] = total; all NW*64 threads
-    __device__ __forceinline__ void block_scan_inplace(uint32_t *a, int m) {
-        constexpr int T = NW * 64;
-        const int per = (m + T - 1) / T;  // consecutive elements per thread
-        const int beg = tid * per;
-        uint32_t loc = 0;
-        for (int q = 0; q < per; ++q)
-            if (beg + q < m) loc += a[beg + q];
-        // wave inclusive scan of loc
-        uint32_t x = loc;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) nw[NW + wave] = x;  // wave totals after the per-wave counts
-        lds_barrier();
-        uint32_t wbase = 0;
-        for (int w2 = 0; w2 < wave; ++w2) wbase += nw[NW + w2];
-        uint32_t run = wbase + x - loc;
-        lds_barrier();  // everyone has read its inputs before they are overwritten
-        for (int q = 0; q < per; ++q) {
-            if (beg + q < m) {
-                const uint32_t v = a[beg + q];
-                a[beg + q] = run;
-                run += v;
-            }
-        }
-        if (tid == T - 1) a[m] = run;
-        lds_barrier();
-    }
-};
-
-// R1 and R3: the piece walk of the dense kernel; SCATTER selects the op.  The
-// scatter variant needs the whole 160 KB LDS (one workgroup per CU).
-template <int K, class Idx, bool SCATTER, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
+// R1: the piece walk of the dense kernel, counting per record piece the windows
+// of each bucket in LDS -> cnt[(s*NBK + b)*G + w].
+template <int K, class Idx>
+__global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
+    constexpr int BLOCK = 1024;
     constexpr int NWAVES = BLOCK / 64;
     constexpr int NBK = 1 << (2 * K - low_bits(K));
-    __shared__ __attribute__((aligned(16))) unsigned long long lds64[NBK];
+    __shared__ uint32_t s_cnt[NBK];
     __shared__ int64_t s_first;
-    uint32_t *lds32 = reinterpret_cast<uint32_t *>(lds64);
-    constexpr int SB = SCATTER ? NWAVES * 1024 * KMC_RSCAT_RT : 1;
-    __shared__ __attribute__((aligned(16))) uint32_t s_srt[SB];
-    __shared__ uint32_t s_off[SCATTER ? NBK + 1 : 1];
-    __shared__ long long s_gdel[SCATTER ? NBK : 1];
-    __shared__ uint32_t s_nw[2 * NWAVES];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -280,41 +114,216 @@ __global__ __launch_bounds__(BLOCK) void radix_pass_kernel(RParams p) {
         const int64_t ps = ca > R0 ? ca : R0;
         const int64_t pe = ce < R1 ? ce : R1;
         if (ps >= pe) continue;
-        const int64_t lbase = (s * NBK) * p.G + w;  // cnt/off index of (s, b=0, w); stride G per bucket
-        for (int b = tid; b < NBK; b += BLOCK) {
-            if (SCATTER) {
-                if (b >= p.b_lo && b < p.b_hi) lds64[b - p.b_lo] = p.off[lbase + (int64_t)b * p.G];
-            } else {
-                lds32[b] = 0u;
-            }
-        }
-        if (SCATTER)
-            for (int b = tid; b <= NBK; b += BLOCK) s_off[b] = 0u;
+        const int64_t lbase = (s * NBK) * p.G + w;  // cnt index of (s, b=0, w); stride G per bucket
+        for (int b = tid; b < NBK; b += BLOCK) s_cnt[b] = 0u;
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
         const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
         const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-        if constexpr (SCATTER) {
-            using Op = RStageOp<K, NWAVES, KMC_RSCAT_RT>;
-            Op op{s_srt, s_off, s_nw, lds64, s_gdel, p.ent, (uint32_t)p.b_lo, (uint32_t)(p.b_hi - p.b_lo),
-                  wave, lane, tid, 0, {}, {}, {}, {}};
-#pragma unroll
-            for (int S = 0; S < KMC_RSCAT_RT; ++S) op.wm[S] = 0u;
-            stream_tiles<K, Op, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
-        } else {
-            RCountOp<K> op{lds32};
-            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
-        }
+        RCountOp<K> op{s_cnt};
+        stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         __syncthreads();
-        if constexpr (!SCATTER) {
-            for (int b = tid; b < NBK; b += BLOCK) p.cnt[lbase + (int64_t)b * p.G] = lds32[b];
-        }
+        for (int b = tid; b < NBK; b += BLOCK) p.cnt[lbase + (int64_t)b * p.G] = s_cnt[b];
         __syncthreads();
     }
 }
 
+// R3: every window's low code bits go to its list (s, bucket) through a ring of
+// RING uint16 entries per bucket in LDS; whenever a 64-byte-aligned segment of the
+// list (32 entries) is complete in a ring it is written out whole.  Each round is
+// one tile per wave (16 K windows):
+//   A  per valid window one returning LDS add on its bucket's word W[b]: the low
+//      16 bits give the window's rank r in this round, the high bits the ring slot
+//      `start` of the bucket's next entry; the entry goes to ring slot
+//      (start + r) mod RING when it fits (r < RING - start % 32: the ring holds
+//      at most 31 carried entries), otherwise straight to its list position
+//      (uncoalesced 2-byte store; only on skewed input);
+//   B  after a barrier, the TPB threads of bucket b (all keeping the bucket's state
+//      in registers: F = global index of its next entry, V = first index still to
+//      be written from the ring) write its complete segments (4 ds_read_b128 +
+//      4 global 16-byte stores each), and thread 0 of the group resets the other
+//      W buffer (W alternates per round, so the reset needs no third barrier).
+// The ring covers list positions [floor32(F), floor32(F) + RING) at the start of a
+// round; positions below V (before this workgroup's segment of the list, or
+// already stored directly) are never written from the ring.  At the end of a piece
+// the partial segment left in the ring is written entry by entry.
+// Per window: 1 returning LDS atomic + 1 ds_write_b16 (the staged counting sort
+// this replaces needed 4 LDS accesses, a block scan and 5 barriers per round),
+// and every global write is a whole 64-byte segment except at list ends.
+template <int K>
+struct RingGeom {
+    static constexpr int LOW = low_bits(K);
+    static constexpr int NBK = 1 << (2 * K - LOW);
+    static constexpr int BLOCK = 1024;
+    static constexpr int TPB = BLOCK / NBK;     // threads per bucket in phase B
+    static constexpr int RING = 65536 / NBK;    // entries per bucket ring (128 KB in all)
+    static constexpr int CH = RING / 8;         // 16-byte chunks per ring
+    static_assert(NBK <= BLOCK && RING >= 64 && (RING & (RING - 1)) == 0, "ring geometry");
+};
+
+// Byte offset in the ring area of entry slot `slot` of bucket b.  16-byte chunks
+// are XOR-swizzled inside a bucket's ring so that the phase-B ds_read_b128 of
+// neighbouring buckets / segments spread over the banks.
+template <int K>
+__device__ __forceinline__ uint32_t ring_off(uint32_t b, uint32_t slot) {
+    using RG = RingGeom<K>;
+    const uint32_t c = slot >> 3;
+    uint32_t t = c ^ ((b >> 1) & (uint32_t)((RG::CH < 8 ? RG::CH : 8) - 1));
+    t ^= (t >> 2) & 3u;
+    return b * (uint32_t)(RG::RING * 2) + t * 16u + (slot & 7u) * 2u;
+}
+
+template <int K>
+struct RRingOp {
+    using RG = RingGeom<K>;
+    static constexpr uint32_t LOWMASK = (1u << RG::LOW) - 1u;
+    char *ring;            // LDS, NBK * RING * 2 bytes
+    uint32_t *W;           // LDS, [2][NBK]
+    unsigned long long *gF;  // LDS, [NBK]: F of every bucket at the start of the round
+    uint16_t *ent;
+    int tid;
+    uint32_t par;          // W buffer of this round
+    // phase-B state of bucket tid / TPB (replicated over its TPB threads)
+    unsigned long long F, V;
+
+    __device__ void before_tile() {}
+
+    template <bool MASKED>
+    __device__ __forceinline__ void tile(uint32_t l, uint32_t h, uint32_t Wm) {
+        uint32_t *w = W + par * RG::NBK;
+        uint32_t old[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t c = window_code_rt<K>(l, h, j);
+            old[j] = 0xFFFFFFFFu;
+            if (!MASKED || ((Wm >> j) & 1u))
+                old[j] = __hip_atomic_fetch_add(&w[c >> RG::LOW], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (old[j] == 0xFFFFFFFFu) continue;
+            const uint32_t c = window_code_rt<K>(l, h, j);
+            const uint32_t b = c >> RG::LOW, e = c & LOWMASK;
+            const uint32_t r = old[j] & 0xFFFFu, st = old[j] >> 16;
+            if (r < (uint32_t)RG::RING - (st & 31u)) {
+                *reinterpret_cast<uint16_t *>(ring + ring_off<K>(b, (st + r) & (RG::RING - 1))) = (uint16_t)e;
+            } else {
+                ent[gF[b] + r] = (uint16_t)e;  // ring full: straight to the list (skewed input)
+            }
+        }
+    }
+
+    // entry at list position g of bucket b, from the ring
+    __device__ __forceinline__ uint16_t ring_entry(uint32_t b, unsigned long long g) const {
+        return *reinterpret_cast<const uint16_t *>(ring + ring_off<K>(b, (uint32_t)g & (RG::RING - 1)));
+    }
+
+    // phase B for this thread's bucket; the caller brackets it with barriers
+    __device__ __forceinline__ void flush() {
+        const uint32_t b = (uint32_t)tid / RG::TPB, j = (uint32_t)tid % RG::TPB;
+        const uint32_t n = W[par * RG::NBK + b] & 0xFFFFu;
+        const unsigned long long F1 = F + n;
+        const unsigned long long H = F & ~31ull;
+        const unsigned long long top = F1 < H + RG::RING ? F1 : H + RG::RING;
+        const uint32_t nseg = (uint32_t)((top - H) >> 5);
+        for (uint32_t i = j; i < nseg; i += RG::TPB) {
+            const unsigned long long g0 = H + 32ull * i;
+            if (g0 >= V) {
+                const uint32_t s0 = (uint32_t)g0 & (RG::RING - 1);
+                const uint4 v0 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0));
+                const uint4 v1 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0 + 8));
+                const uint4 v2 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0 + 16));
+                const uint4 v3 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0 + 24));
+                uint4 *dst = reinterpret_cast<uint4 *>(ent + g0);
+                dst[0] = v0;
+                dst[1] = v1;
+                dst[2] = v2;
+                dst[3] = v3;
+            } else {
+                for (uint32_t q = 0; q < 32; ++q)
+                    if (g0 + q >= V) ent[g0 + q] = ring_entry(b, g0 + q);
+            }
+        }
+        if (F1 > H + RG::RING) V = F1;  // [H + RING, F1) went straight to the list
+        F = F1;
+        if (j == 0) {
+            W[(par ^ 1u) * RG::NBK + b] = ((uint32_t)F1 & (RG::RING - 1)) << 16;
+            gF[b] = F1;
+        }
+        par ^= 1u;
+    }
+
+    __device__ void after_iter(int64_t, int64_t, bool) {
+        lds_barrier();  // every window of the round is ranked and in its ring
+        flush();
+        lds_barrier();  // rings read, W reset: the next round may write
+    }
+
+    // end of a piece: the partial segment left in the ring, entry by entry
+    __device__ __forceinline__ void finish() {
+        const uint32_t b = (uint32_t)tid / RG::TPB, j = (uint32_t)tid % RG::TPB;
+        const unsigned long long H = F & ~31ull;
+        const unsigned long long lo = H > V ? H : V;
+        for (unsigned long long g = lo + j; g < F; g += RG::TPB) ent[g] = ring_entry(b, g);
+    }
+};
+
+// R3 launch: the piece walk of radix_count_kernel with the ring scatter (the whole
+// LDS of a CU: one 1024-thread workgroup per CU).
+template <int K, class Idx>
+__global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
+    using RG = RingGeom<K>;
+    constexpr int NWAVES = RG::BLOCK / 64;
+    __shared__ __attribute__((aligned(16))) char s_ring[RG::NBK * RG::RING * 2];
+    __shared__ uint32_t s_W[2 * RG::NBK];
+    __shared__ unsigned long long s_gF[RG::NBK];
+    __shared__ int64_t s_first;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w = blockIdx.x;
+    const Geom g = make_geom<Idx>(p);
+    const int64_t tb = g.T0 + (int64_t)w * g.tpw;
+    const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
+    if (tb >= te) return;
+    const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
+    const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
+    if (tid == 0) s_first = first_record_at<Idx>(p, R0);
+    __syncthreads();
+    const uint32_t b = (uint32_t)tid / RG::TPB;
+    for (int64_t s = s_first; s < p.n; ++s) {
+        if (rec_off<Idx>(p, s) >= R1) break;
+        int64_t ca, ce;
+        record_windows<K, Idx>(p, g, s, ca, ce);
+        const int64_t ps = ca > R0 ? ca : R0;
+        const int64_t pe = ce < R1 ? ce : R1;
+        if (ps >= pe) continue;
+        RRingOp<K> op;
+        op.ring = s_ring;
+        op.W = s_W;
+        op.gF = s_gF;
+        op.ent = p.ent;
+        op.tid = tid;
+        op.par = 0;
+        op.F = p.off[((s * RG::NBK) + b) * p.G + w];  // this workgroup's segment of list (s, b)
+        op.V = op.F;
+        if ((uint32_t)tid % RG::TPB == 0) {
+            s_W[b] = ((uint32_t)op.F & (RG::RING - 1)) << 16;
+            s_gF[b] = op.F;
+        }
+        __syncthreads();
+        const int64_t tp0 = ps >> kTileShift;
+        const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
+        const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
+        const int64_t a0 = tp0 + (int64_t)wave * per;
+        const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
+        stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        op.finish();
+        __syncthreads();
+    }
+}
 
 // R4: one workgroup per list (s, b).
 template <int LOW>
@@ -446,13 +455,6 @@ __global__ __launch_bounds__(256) void radix_invalid_kernel(RParams p) {
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
-constexpr int kPassBlock = 1024;
-// target footprint of the list lines one R3 launch keeps open (G x buckets x 128 B)
-#ifndef KMC_OPEN_LIST_MB
-#define KMC_OPEN_LIST_MB 64
-#endif
-constexpr size_t kOpenListBytes = (size_t)KMC_OPEN_LIST_MB << 20;
-
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct RLayout {
@@ -551,8 +553,6 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     p.derive = 0;
     p.G = G;
     p.nbk = 1 << (2 * K - low_bits(K));
-    p.b_lo = 0;
-    p.b_hi = p.nbk;
     p.cnt = reinterpret_cast<uint32_t *>(base + L.cnt);
     p.off = reinterpret_cast<uint64_t *>(base + L.off);
     p.ent = reinterpret_cast<uint16_t *>(base + L.ent);
@@ -569,16 +569,9 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     }
     he = hipMemsetAsync(p.cnt, 0, (size_t)L.m * 4, st);
     if (he != hipSuccess) return (int)he;
-    hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, false, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
+    hipLaunchKernelGGL((radix_count_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
     excl_scan_u32(p.cnt, L.m, bsum, p.off, st);
-    // R3 in bucket groups whose open lines (G x buckets x 128 B) fit kOpenListBytes
-    int groups = 1;
-    while ((size_t)G * (size_t)(p.nbk / groups) * 128 > kOpenListBytes && groups < p.nbk) groups *= 2;
-    for (int gi = 0; gi < groups; ++gi) {
-        p.b_lo = gi * (p.nbk / groups);
-        p.b_hi = p.b_lo + p.nbk / groups;
-        hipLaunchKernelGGL((radix_pass_kernel<K, int64_t, true, kPassBlock>), dim3(G), dim3(kPassBlock), 0, st, p);
-    }
+    hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
     hipLaunchKernelGGL((radix_hist_kernel<low_bits(K)>), dim3((unsigned)std::min<int64_t>(n * p.nbk, kMaxGridX)),
                        dim3(1024), 0, st, p, nbins);
     hipLaunchKernelGGL(radix_place_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st, p, nbins);
