@@ -69,10 +69,14 @@ struct RParams {
     int32_t *invalid;
 };
 
+// R1 op: bucket counters with kCountRep replicas interleaved (counter b of lane l
+// at word b*kCountRep + l % kCountRep), so the 32 lanes of an LDS lane group
+// always hit 32 different banks (1 024 buckets x 32 replicas = 128 KB at k = 13).
+constexpr int kCountRep = 32;
 template <int K>
 struct RCountOp {
     static constexpr int LOW = low_bits(K);
-    uint32_t *c;  // LDS bucket counters
+    uint32_t *c;  // LDS bucket counters (this lane's replica)
     __device__ void before_tile() {}
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
@@ -80,7 +84,8 @@ struct RCountOp {
         for (int j = 0; j < 16; ++j) {
             const uint32_t code = window_code_rt<K>(lo, hi, j);
             if (!MASKED || ((W >> j) & 1u))
-                __hip_atomic_fetch_add(&c[code >> LOW], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&c[(code >> LOW) * kCountRep], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __device__ void after_iter(int64_t, int64_t, bool) {}
@@ -93,7 +98,7 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
     constexpr int BLOCK = 1024;
     constexpr int NWAVES = BLOCK / 64;
     constexpr int NBK = 1 << (2 * K - low_bits(K));
-    __shared__ uint32_t s_cnt[NBK];
+    __shared__ uint32_t s_cnt[NBK * kCountRep];
     __shared__ int64_t s_first;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -115,17 +120,26 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
         const int64_t pe = ce < R1 ? ce : R1;
         if (ps >= pe) continue;
         const int64_t lbase = (s * NBK) * p.G + w;  // cnt index of (s, b=0, w); stride G per bucket
-        for (int b = tid; b < NBK; b += BLOCK) s_cnt[b] = 0u;
+        for (int i = tid; i < NBK * kCountRep; i += BLOCK) s_cnt[i] = 0u;
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
         const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
         const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-        RCountOp<K> op{s_cnt};
+        RCountOp<K> op{s_cnt + (lane & (kCountRep - 1))};
         stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         __syncthreads();
-        for (int b = tid; b < NBK; b += BLOCK) p.cnt[lbase + (int64_t)b * p.G] = s_cnt[b];
+        for (int b = tid; b < NBK; b += BLOCK) {
+            const uint4 *r4 = reinterpret_cast<const uint4 *>(s_cnt + b * kCountRep);
+            uint32_t t = 0u;
+#pragma unroll
+            for (int q = 0; q < kCountRep / 4; ++q) {
+                const uint4 v = r4[(q + b) & (kCountRep / 4 - 1)];  // rotated: spread the banks
+                t += v.x + v.y + v.z + v.w;
+            }
+            p.cnt[lbase + (int64_t)b * p.G] = t;
+        }
         __syncthreads();
     }
 }
@@ -134,21 +148,26 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
 // RING uint16 entries per bucket in LDS; whenever a 64-byte-aligned segment of the
 // list (32 entries) is complete in a ring it is written out whole.  Each round is
 // one tile per wave (16 K windows):
-//   A  per valid window one returning LDS add on its bucket's word W[b]: the low
-//      16 bits give the window's rank r in this round, the high bits the ring slot
-//      `start` of the bucket's next entry; the entry goes to ring slot
-//      (start + r) mod RING when it fits (r < RING - start % 32: the ring holds
-//      at most 31 carried entries), otherwise straight to its list position
-//      (uncoalesced 2-byte store; only on skewed input);
+//   A  per valid window one returning LDS add on its bucket's word W[b], which
+//      holds (halfword address of the bucket's current ring half) << 16 | (fill
+//      of the ring's current 32-entry segment + windows ranked so far): the
+//      returned value gives the entry's LDS address in three VALU ops and whether
+//      it fits (low half < RING: the ring holds at most 31 carried entries).  The
+//      ds_write_b16 is unconditional (windows that are invalid or do not fit write
+//      a per-lane dummy word); entries that do not fit go straight to their list
+//      position in a cold path (uncoalesced 2-byte stores; skewed input only);
 //   B  after a barrier, the TPB threads of bucket b (all keeping the bucket's state
-//      in registers: F = global index of its next entry, V = first index still to
-//      be written from the ring) write its complete segments (4 ds_read_b128 +
-//      4 global 16-byte stores each), and thread 0 of the group resets the other
-//      W buffer (W alternates per round, so the reset needs no third barrier).
-// The ring covers list positions [floor32(F), floor32(F) + RING) at the start of a
-// round; positions below V (before this workgroup's segment of the list, or
-// already stored directly) are never written from the ring.  At the end of a piece
-// the partial segment left in the ring is written entry by entry.
+//      in registers: F = list index of its next entry, V = first index still to be
+//      written from the ring) write its complete segments (4 ds_read_b128 + 4
+//      global 16-byte stores each), and thread 0 of the group sets up the other W
+//      buffer (W alternates per round, so the reset needs no third barrier).
+// List position g of bucket b lives in ring slot (g + rot(b)) mod RING: the
+// per-bucket rotation (a multiple of 8 slots) spreads the phase-B 16-byte reads of
+// neighbouring buckets over the banks, and the TPB threads of one bucket read
+// their segments' chunks in rotated order for the same reason.  Positions below V
+// (before this workgroup's segment of the list, or already stored directly) are
+// never written from the ring.  At the end of a piece the partial segment left in
+// a ring is written entry by entry.
 // Per window: 1 returning LDS atomic + 1 ds_write_b16 (the staged counting sort
 // this replaces needed 4 LDS accesses, a block scan and 5 barriers per round),
 // and every global write is a whole 64-byte segment except at list ends.
@@ -163,27 +182,29 @@ struct RingGeom {
     static_assert(NBK <= BLOCK && RING >= 64 && (RING & (RING - 1)) == 0, "ring geometry");
 };
 
-// Byte offset in the ring area of entry slot `slot` of bucket b.  16-byte chunks
-// are XOR-swizzled inside a bucket's ring so that the phase-B ds_read_b128 of
-// neighbouring buckets / segments spread over the banks.
 template <int K>
-__device__ __forceinline__ uint32_t ring_off(uint32_t b, uint32_t slot) {
+__device__ __forceinline__ uint32_t ring_rot(uint32_t b) {
+    return ((b >> 1) & 7u) * 8u;
+}
+
+// W word of bucket b for a round that starts at list index F
+template <int K>
+__device__ __forceinline__ uint32_t ring_word(uint32_t b, unsigned long long F) {
     using RG = RingGeom<K>;
-    const uint32_t c = slot >> 3;
-    uint32_t t = c ^ ((b >> 1) & (uint32_t)((RG::CH < 8 ? RG::CH : 8) - 1));
-    t ^= (t >> 2) & 3u;
-    return b * (uint32_t)(RG::RING * 2) + t * 16u + (slot & 7u) * 2u;
+    const uint32_t f0 = (uint32_t)F & 31u;
+    const uint32_t half = ((uint32_t)F - f0 + ring_rot<K>(b)) & (uint32_t)(RG::RING - 1);
+    return ((b * (uint32_t)RG::RING + half) << 16) | f0;
 }
 
 template <int K>
 struct RRingOp {
     using RG = RingGeom<K>;
-    static constexpr uint32_t LOWMASK = (1u << RG::LOW) - 1u;
-    char *ring;            // LDS, NBK * RING * 2 bytes
+    uint16_t *ring;        // LDS, NBK * RING entries
     uint32_t *W;           // LDS, [2][NBK]
-    unsigned long long *gF;  // LDS, [NBK]: F of every bucket at the start of the round
+    unsigned long long *gH;  // LDS, [NBK]: floor32(F) of every bucket at the start of the round
+    uint16_t *dummy;       // LDS, 2 halfwords per lane
     uint16_t *ent;
-    int tid;
+    int tid, lane;
     uint32_t par;          // W buffer of this round
     // phase-B state of bucket tid / TPB (replicated over its TPB threads)
     unsigned long long F, V;
@@ -196,51 +217,68 @@ struct RRingOp {
         uint32_t old[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const uint32_t c = window_code_rt<K>(l, h, j);
-            old[j] = 0xFFFFFFFFu;
+            const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);  // low 2k bits: the window
+            old[j] = 0u;
             if (!MASKED || ((Wm >> j) & 1u))
-                old[j] = __hip_atomic_fetch_add(&w[c >> RG::LOW], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old[j] = __hip_atomic_fetch_add(&w[(c >> RG::LOW) & (RG::NBK - 1)], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        uint32_t worst = 0u;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            if (old[j] == 0xFFFFFFFFu) continue;
-            const uint32_t c = window_code_rt<K>(l, h, j);
-            const uint32_t b = c >> RG::LOW, e = c & LOWMASK;
-            const uint32_t r = old[j] & 0xFFFFu, st = old[j] >> 16;
-            if (r < (uint32_t)RG::RING - (st & 31u)) {
-                *reinterpret_cast<uint16_t *>(ring + ring_off<K>(b, (st + r) & (RG::RING - 1))) = (uint16_t)e;
-            } else {
-                ent[gF[b] + r] = (uint16_t)e;  // ring full: straight to the list (skewed input)
+            const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);
+            const uint32_t lo = old[j] & 0xFFFFu, hi = old[j] >> 16;
+            // halfword index: the ring half's base with the in-ring offset wrapped
+            const uint32_t hw = (hi & ~(uint32_t)(RG::RING - 1)) | ((hi + lo) & (uint32_t)(RG::RING - 1));
+            bool ok = lo < (uint32_t)RG::RING;
+            if (MASKED) ok = ok && ((Wm >> j) & 1u);
+            uint16_t *dst = ok ? ring + hw : dummy + 2 * lane;
+            // the entry: the low LOW bits (ds_write_b16 drops the rest when LOW = 16)
+            *dst = (uint16_t)(RG::LOW == 16 ? c : c & ((1u << RG::LOW) - 1u));
+            if (!MASKED || ((Wm >> j) & 1u)) worst = lo > worst ? lo : worst;
+        }
+        if (__builtin_expect(__any(worst >= (uint32_t)RG::RING), 0)) {
+            // ring full: straight to the list (skewed input)
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);
+                const uint32_t lo = old[j] & 0xFFFFu;
+                if ((!MASKED || ((Wm >> j) & 1u)) && lo >= (uint32_t)RG::RING)
+                    ent[gH[(c >> RG::LOW) & (RG::NBK - 1)] + lo] = (uint16_t)(c & ((1u << RG::LOW) - 1u));
             }
         }
     }
 
     // entry at list position g of bucket b, from the ring
     __device__ __forceinline__ uint16_t ring_entry(uint32_t b, unsigned long long g) const {
-        return *reinterpret_cast<const uint16_t *>(ring + ring_off<K>(b, (uint32_t)g & (RG::RING - 1)));
+        return ring[b * RG::RING + (((uint32_t)g + ring_rot<K>(b)) & (RG::RING - 1))];
     }
 
     // phase B for this thread's bucket; the caller brackets it with barriers
     __device__ __forceinline__ void flush() {
         const uint32_t b = (uint32_t)tid / RG::TPB, j = (uint32_t)tid % RG::TPB;
-        const uint32_t n = W[par * RG::NBK + b] & 0xFFFFu;
+        const uint32_t f0 = (uint32_t)F & 31u;
+        const uint32_t n = (W[par * RG::NBK + b] & 0xFFFFu) - f0;
         const unsigned long long F1 = F + n;
-        const unsigned long long H = F & ~31ull;
+        const unsigned long long H = F - f0;
         const unsigned long long top = F1 < H + RG::RING ? F1 : H + RG::RING;
         const uint32_t nseg = (uint32_t)((top - H) >> 5);
+        const uint32_t rot = ring_rot<K>(b);
+        const uint4 *row = reinterpret_cast<const uint4 *>(ring + b * RG::RING);
         for (uint32_t i = j; i < nseg; i += RG::TPB) {
             const unsigned long long g0 = H + 32ull * i;
             if (g0 >= V) {
-                const uint32_t s0 = (uint32_t)g0 & (RG::RING - 1);
-                const uint4 v0 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0));
-                const uint4 v1 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0 + 8));
-                const uint4 v2 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0 + 16));
-                const uint4 v3 = *reinterpret_cast<const uint4 *>(ring + ring_off<K>(b, s0 + 24));
+                const uint32_t c0 = (((uint32_t)g0 + rot) & (RG::RING - 1)) >> 3;  // first 16-byte chunk
+                const uint32_t sh = (i >> 2) & 3u;  // rotated chunk order: TPB readers of one ring
                 uint4 *dst = reinterpret_cast<uint4 *>(ent + g0);
-                dst[0] = v0;
-                dst[1] = v1;
-                dst[2] = v2;
-                dst[3] = v3;
+                const uint32_t q0 = sh, q1 = (sh + 1) & 3u, q2 = (sh + 2) & 3u, q3 = (sh + 3) & 3u;
+                const uint4 v0 = row[(c0 + q0) & (RG::CH - 1)];
+                const uint4 v1 = row[(c0 + q1) & (RG::CH - 1)];
+                const uint4 v2 = row[(c0 + q2) & (RG::CH - 1)];
+                const uint4 v3 = row[(c0 + q3) & (RG::CH - 1)];
+                dst[q0] = v0;
+                dst[q1] = v1;
+                dst[q2] = v2;
+                dst[q3] = v3;
             } else {
                 for (uint32_t q = 0; q < 32; ++q)
                     if (g0 + q >= V) ent[g0 + q] = ring_entry(b, g0 + q);
@@ -249,8 +287,8 @@ struct RRingOp {
         if (F1 > H + RG::RING) V = F1;  // [H + RING, F1) went straight to the list
         F = F1;
         if (j == 0) {
-            W[(par ^ 1u) * RG::NBK + b] = ((uint32_t)F1 & (RG::RING - 1)) << 16;
-            gF[b] = F1;
+            W[(par ^ 1u) * RG::NBK + b] = ring_word<K>(b, F1);
+            gH[b] = F1 & ~31ull;
         }
         par ^= 1u;
     }
@@ -258,7 +296,7 @@ struct RRingOp {
     __device__ void after_iter(int64_t, int64_t, bool) {
         lds_barrier();  // every window of the round is ranked and in its ring
         flush();
-        lds_barrier();  // rings read, W reset: the next round may write
+        lds_barrier();  // rings read, W set up: the next round may write
     }
 
     // end of a piece: the partial segment left in the ring, entry by entry
@@ -276,9 +314,10 @@ template <int K, class Idx>
 __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
     using RG = RingGeom<K>;
     constexpr int NWAVES = RG::BLOCK / 64;
-    __shared__ __attribute__((aligned(16))) char s_ring[RG::NBK * RG::RING * 2];
+    __shared__ __attribute__((aligned(16))) uint16_t s_ring[RG::NBK * RG::RING];
     __shared__ uint32_t s_W[2 * RG::NBK];
-    __shared__ unsigned long long s_gF[RG::NBK];
+    __shared__ unsigned long long s_gH[RG::NBK];
+    __shared__ uint16_t s_dummy[128];
     __shared__ int64_t s_first;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -303,15 +342,17 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         RRingOp<K> op;
         op.ring = s_ring;
         op.W = s_W;
-        op.gF = s_gF;
+        op.gH = s_gH;
+        op.dummy = s_dummy;
         op.ent = p.ent;
         op.tid = tid;
+        op.lane = lane;
         op.par = 0;
         op.F = p.off[((s * RG::NBK) + b) * p.G + w];  // this workgroup's segment of list (s, b)
         op.V = op.F;
         if ((uint32_t)tid % RG::TPB == 0) {
-            s_W[b] = ((uint32_t)op.F & (RG::RING - 1)) << 16;
-            s_gF[b] = op.F;
+            s_W[b] = ring_word<K>(b, op.F);
+            s_gH[b] = op.F & ~31ull;
         }
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
@@ -354,17 +395,45 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
     if (a < end) {
         const uint64_t nvec = (end - a) / 8;
         const uint4 *v = reinterpret_cast<const uint4 *>(ent + a);
-        for (uint64_t i = threadIdx.x; i < nvec; i += 1024) {
-            const uint4 x = v[i];
-            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                add(w[q] & 0xFFFFu);
-                add(w[q] >> 16);
-            }
+        const auto add8 = [&](const uint4 x) {
+            add(x.x & 0xFFFFu);
+            add(x.x >> 16);
+            add(x.y & 0xFFFFu);
+            add(x.y >> 16);
+            add(x.z & 0xFFFFu);
+            add(x.z >> 16);
+            add(x.w & 0xFFFFu);
+            add(x.w >> 16);
+        };
+        // four 16-byte loads in flight per lane (64 KB per CU): one per iteration
+        // left the loop waiting on HBM latency
+        uint64_t i = threadIdx.x;
+        for (; i + 3 * 1024 < nvec; i += 4 * 1024) {
+            const uint4 x0 = v[i], x1 = v[i + 1024], x2 = v[i + 2048], x3 = v[i + 3072];
+            add8(x0);
+            add8(x1);
+            add8(x2);
+            add8(x3);
         }
+        for (; i < nvec; i += 1024) add8(v[i]);
         const uint64_t t = a + nvec * 8;
         if (t + threadIdx.x < end) add(ent[t + threadIdx.x]);
+    }
+}
+
+// Cold path of R4 (LOW = 16): the list recounted exactly in two 32 768-bin
+// halves with 32-bit bins (kept out of line: the hot loop's registers).
+template <int LOW>
+__device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uint64_t end, uint32_t *h,
+                                          uint32_t *dst) {
+    constexpr int kWords = 1 << (LOW - 1);
+    for (uint32_t half = 0; half < 2; ++half) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+        __syncthreads();
+        hist_list<LOW, true>(ent, beg, end, h, half);
+        __syncthreads();
+        for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
     }
 }
 
@@ -402,14 +471,7 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
                     reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
                 }
             } else {  // a bin wrapped: exact recount, half of the bins at a time
-                for (uint32_t half = 0; half < 2; ++half) {
-                    __syncthreads();
-                    for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
-                    __syncthreads();
-                    hist_list<LOW, true>(p.ent, beg, end, h, half);
-                    __syncthreads();
-                    for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
-                }
+                hist_recount<LOW>(p.ent, beg, end, h, dst);
             }
         }
         __syncthreads();  // h and s_sum are reused by the next list
