@@ -35,6 +35,10 @@
 #ifndef KMC_RSCAT_PF
 #define KMC_RSCAT_PF 2
 #endif
+// tiles per wave in one R3 ring round (more: fewer barriers, more ring overflows)
+#ifndef KMC_RING_RT
+#define KMC_RING_RT 1
+#endif
 
 namespace kmc {
 namespace {
@@ -223,21 +227,23 @@ struct RRingOp {
                 old[j] = __hip_atomic_fetch_add(&w[(c >> RG::LOW) & (RG::NBK - 1)], 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        uint32_t worst = 0u;
+        uint32_t any = 0u;  // OR of the returned words: low half >= RING iff some entry did not fit
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);
-            const uint32_t lo = old[j] & 0xFFFFu, hi = old[j] >> 16;
-            // halfword index: the ring half's base with the in-ring offset wrapped
-            const uint32_t hw = (hi & ~(uint32_t)(RG::RING - 1)) | ((hi + lo) & (uint32_t)(RG::RING - 1));
-            bool ok = lo < (uint32_t)RG::RING;
+            const uint32_t hi = old[j] >> 16;
+            // halfword index: the ring half's base (hi) with the in-ring offset
+            // (hi + lo) mod RING inserted (one v_bfi); hi + old has the same low bits
+            const uint32_t hw = __builtin_amdgcn_ubfe(hi + old[j], 0, 31) & (uint32_t)(RG::RING - 1);
+            const uint32_t idx = hw | (hi & ~(uint32_t)(RG::RING - 1));
+            bool ok = (old[j] & 0xFFFFu) < (uint32_t)RG::RING;
             if (MASKED) ok = ok && ((Wm >> j) & 1u);
-            uint16_t *dst = ok ? ring + hw : dummy + 2 * lane;
+            uint16_t *dst = ok ? ring + idx : dummy + 2 * lane;
             // the entry: the low LOW bits (ds_write_b16 drops the rest when LOW = 16)
             *dst = (uint16_t)(RG::LOW == 16 ? c : c & ((1u << RG::LOW) - 1u));
-            if (!MASKED || ((Wm >> j) & 1u)) worst = lo > worst ? lo : worst;
+            any |= old[j];
         }
-        if (__builtin_expect(__any(worst >= (uint32_t)RG::RING), 0)) {
+        if (__builtin_expect(__any((any & 0xFFFFu) >= (uint32_t)RG::RING), 0)) {
             // ring full: straight to the list (skewed input)
             for (int j = 0; j < 16; ++j) {
                 const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);
@@ -293,7 +299,11 @@ struct RRingOp {
         par ^= 1u;
     }
 
-    __device__ void after_iter(int64_t, int64_t, bool) {
+    int held = 0;  // tiles of this round taken (workgroup-uniform)
+
+    __device__ void after_iter(int64_t i, int64_t per, bool) {
+        if (++held < KMC_RING_RT && i + 1 < per) return;
+        held = 0;
         lds_barrier();  // every window of the round is ranked and in its ring
         flush();
         lds_barrier();  // rings read, W set up: the next round may write
@@ -478,13 +488,30 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
     }
 }
 
-// R5: stage [n][nbins] -> sum[s + ld*code]; one workgroup per 256 codes.
+// R5: stage [n][nbins] -> sum[s + ld*code], transposed through LDS in tiles of
+// kPlaceS records x kPlaceC codes: rows are read 16 bytes per lane, and the
+// tile's output (kPlaceC codes x its records) is written in record-fastest order,
+// i.e. contiguously when ld = n.  Grid (nbins / kPlaceC, record groups).
+constexpr int kPlaceC = 512, kPlaceS = 16;
 __global__ __launch_bounds__(256) void radix_place_kernel(RParams p, int64_t nbins) {
-    const int64_t c0 = (int64_t)blockIdx.x * 256;
-    const int64_t total = 256 * p.n;  // outputs of this block: codes c0..c0+255, all records
-    for (int64_t i = threadIdx.x; i < total; i += 256) {
-        const int64_t c = c0 + i / p.n, s = i % p.n;  // consecutive threads -> consecutive records
-        if (c < nbins) p.sum[s + p.ld * c] = (int32_t)p.stage[s * nbins + c];
+    __shared__ uint32_t t[kPlaceS][kPlaceC + 1];
+    const int64_t c0 = (int64_t)blockIdx.x * kPlaceC;
+    for (int64_t s0 = (int64_t)blockIdx.y * kPlaceS; s0 < p.n; s0 += (int64_t)gridDim.y * kPlaceS) {
+        const int ts = (int)(p.n - s0 < kPlaceS ? p.n - s0 : kPlaceS);
+        for (int q = threadIdx.x; q < ts * (kPlaceC / 4); q += 256) {
+            const int r = q / (kPlaceC / 4), cc = (q % (kPlaceC / 4)) * 4;
+            const uint4 v = *reinterpret_cast<const uint4 *>(p.stage + (s0 + r) * nbins + c0 + cc);
+            t[r][cc] = v.x;
+            t[r][cc + 1] = v.y;
+            t[r][cc + 2] = v.z;
+            t[r][cc + 3] = v.w;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < ts * kPlaceC; i += 256) {
+            const int c = i / ts, r = i % ts;
+            p.sum[s0 + r + p.ld * (c0 + c)] = (int32_t)t[r][c];
+        }
+        __syncthreads();
     }
 }
 
@@ -636,7 +663,10 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
     hipLaunchKernelGGL((radix_hist_kernel<low_bits(K)>), dim3((unsigned)std::min<int64_t>(n * p.nbk, kMaxGridX)),
                        dim3(1024), 0, st, p, nbins);
-    hipLaunchKernelGGL(radix_place_kernel, dim3((unsigned)((nbins + 255) / 256)), dim3(256), 0, st, p, nbins);
+    hipLaunchKernelGGL(radix_place_kernel,
+                       dim3((unsigned)(nbins / kPlaceC), (unsigned)std::min<int64_t>((n + kPlaceS - 1) / kPlaceS,
+                                                                                     kMaxGridY)),
+                       dim3(256), 0, st, p, nbins);
     if (t_trace_after) {
         he = hipEventRecord(t_trace_after, st);
         if (he != hipSuccess) return (int)he;

@@ -4,6 +4,8 @@ bench.py times configs[1], the headline):
   C3  10 Gbase synthetic, k = 13 dense histogram (radix path), whole call timed
   C4  GRCh38-sized synthetic (3.1 Gbase, 25 chromosome-like records, ~5 % N runs,
       ~50 % soft-masked lowercase), k = 31 canonical counting with KMC_CANON_SOFTMASK
+  C4R the same size and k, repeat-rich (scripts/genome_synth.py: interspersed and
+      tandem repeats, reverse-complemented copies, soft-masked repeats)
 Input resident in HBM; one JSON line per configuration.
 Usage: python scripts/cbench.py [--configs c3,c4] [--iters 3] [--gbases-c4 3.1]"""
 import argparse
@@ -13,6 +15,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dna-kmeres-parallel_amd"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def grch38_like(torch, dev, gbases, seed=38):
@@ -209,7 +212,7 @@ def timed(torch, fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c4")
+    ap.add_argument("--configs", default="c3,c4,c4r")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--gbases-c3", type=float, default=10.0)
     ap.add_argument("--gbases-c4", type=float, default=3.1)
@@ -245,8 +248,17 @@ def main():
         print(json.dumps(line), flush=True)
         del data, out, ws, args
         torch.cuda.empty_cache()
-    if "c4" in cfgs:
-        data, idx, lens = grch38_like(torch, dev, a.gbases_c4)
+    for cfg in [c for c in cfgs if c in ("c4", "c4r")]:
+        if cfg == "c4":
+            data, idx, lens = grch38_like(torch, dev, a.gbases_c4)
+            extra = {"input": "iid ACGT, 5 % N runs, 50 % soft-masked runs (no repeats)"}
+        else:  # repeat-rich stand-in (scripts/genome_synth.py)
+            import genome_synth
+            t0 = time.perf_counter()
+            data, idx, lens, st = genome_synth.repeat_genome(torch, dev, a.gbases_c4)
+            torch.cuda.synchronize()
+            extra = {"input": "repeat-rich synthetic genome (scripts/genome_synth.py)", "composition": st,
+                     "gen_s": time.perf_counter() - t0}
         k = 31
         kmers = sum(max(0, L - k + 1) for L in lens)
         res = {}
@@ -258,14 +270,20 @@ def main():
         keys, counts, off = res["r"]
         tot = int(counts.sum().item())
         alg = 17 * kmers  # 1 B input + 16 B table slot per k-mer
-        line = {"config": "C4", "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
+        line = {"config": cfg.upper(), "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
                 "valid_windows": tot, "distinct": int(keys.numel()), "s_med": med, "s_min": best,
                 "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9, "frac8TB": alg / med / 8e12}
+        line.update(extra)
+        line["max_count"] = int(counts.max().item())
+        line["keys_count_gt1"] = int((counts > 1).sum().item())
         if a.check:
             line["parity"] = check_c4(torch, kmc, data, idx, k, keys, counts, off)
         if a.cpu_sample_c4 > 0:
             line["cpu_baseline"] = c4_cpu_baseline(data, idx, k, a.cpu_sample_c4)
         print(json.dumps(line), flush=True)
+        del data, idx, keys, counts, off
+        res.clear()
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

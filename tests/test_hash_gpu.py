@@ -165,3 +165,25 @@ def test_canonical_capacity_error(kmc, cuda):
     assert ei.value.code == 1009
     with pytest.raises(kmc.KmcError):
         kmc.count_canonical(d, dev(idx, cuda), 32)
+
+
+@pytest.mark.parametrize("k,soft", [(31, True), (21, True), (31, False), (15, True)])
+def test_canonical_repeat_rich_genome(kmc, oracle, cuda, k, soft):
+    """The repeat-rich synthetic genome of config C4 (scripts/genome_synth.py: ~45 %
+    interspersed repeats with 0-15 % divergence, half reverse-complemented,
+    tandem repeats, N runs, soft-masked repeats) at 40 Mbase in 25 records: many
+    keys occur thousands of times (the LDS table's repeat path, hot keys within
+    a pass) and reverse-complement copies fold onto shared keys."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import genome_synth
+    data, idx, _, _ = genome_synth.repeat_genome(torch, cuda, 0.04, seed=77, min_len=20_000)
+    host, hidx = data.cpu().numpy(), idx.cpu().numpy()
+    flags = kmc.CANON_SOFTMASK if soft else 0
+    got = gpu_canon(kmc, cuda, host, hidx, k, flags)
+    exp = oracle.count_canonical(host, hidx, k, soft=soft)
+    if soft:  # the repeat path is exercised (unmasked: the lowercase repeats are not bases)
+        assert exp[1].max() > 1000 and (exp[1] > 1).sum() > 100_000
+    assert_same(got, exp, "repeat-rich k=%d soft=%s" % (k, soft))
