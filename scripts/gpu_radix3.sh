@@ -1,13 +1,13 @@
 # GPU: radix-path parity (default build), C3 under a kernel trace, then C3 (with
 # its parity check) for every diagnostic build in lib/variants/.
-cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/radix3 && mkdir -p $O && rm -rf $O/*
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/${RADIX_OUT:-radix3} && mkdir -p $O && rm -rf $O/*
 timeout -k 10 600 python -u -m pytest tests/test_dense_gpu.py -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k "${TK:-radix or golden or many or shards or bench_rank}" > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log; if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED" $O/tests.log | head -20; exit $rc; fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/cb -o cb -- python3 scripts/cbench.py --configs c3 --iters 5 --cpu-sample-c3 0 > $O/cb.log 2>&1 || { tail -20 $O/cb.log; exit 1; }
 grep '^{' $O/cb.log | cut -c1-220
 python3 - <<'PY'
 import csv, glob
-f = glob.glob("gpurun_out/radix3/cb/**/*kernel_stats.csv", recursive=True)[0]
+f = glob.glob("gpurun_out/*/cb/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
     n = r["Name"].replace("(anonymous namespace)::", "").replace("kmc::", "")
     if "at::" in n or "rocprim" in n or "rocclr" in n: continue
