@@ -64,7 +64,7 @@ struct Params {
     int64_t wl, wh, rl, rh;  // window range, readable range (derive == 0)
     int derive;              // 1: both ranges = [indices[0], indices[n])
     int G;                   // workgroups of the count kernel
-    uint32_t *slab;          // [G][2][4^k]
+    uint32_t *slab;          // [G][2][4^k] (k = 8: the first 4^k / 2 words, packed 16-bit halves)
     int64_t *slot_rec;       // [G][2] record held by each slab slot, -1 = none
     Spill *spill;            // [G][spill_cap]
     uint32_t *spill_cnt;     // [G]
@@ -455,8 +455,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                         p.sum[s + p.ld * (int64_t)i] = (int32_t)(v & 0xFFFFu);
                         p.sum[s + p.ld * (int64_t)(i + NW)] = (int32_t)(v >> 16);
                     } else {
-                        dst[i] = v & 0xFFFFu;
-                        dst[i + NW] = v >> 16;
+                        dst[i] = v;  // packed as in LDS: the halves are exact (wraps live in spills)
                     }
                 }
                 if constexpr (HM == 3) {
@@ -502,31 +501,45 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
 }
 
 // Records that span several workgroups: sum their slab slots; records without a
-// window in range get zeros.  Grid (ceil(4^k / 256), ny): blockIdx.x picks 256
-// codes, records s = blockIdx.y, blockIdx.y + ny, ... (the record count is not
-// bounded by the grid: gridDim.x * blockDim.x stays far below 2^32).
-template <int K, class Idx>
+// window in range get zeros.  Grid (ceil(W / 256), ny): blockIdx.x picks 256
+// slab words (W = 4^k, or 4^k / 2 packed words at k = 8, each holding bins c and
+// c | 0x8000), records s = blockIdx.y, blockIdx.y + ny, ... (the record count is
+// not bounded by the grid: gridDim.x * blockDim.x stays far below 2^32).
+template <int K, class Idx, bool P16>
 __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     constexpr int NB = 1 << (2 * K);
+    constexpr int NW = P16 ? NB / 2 : NB;
     const int c = (int)blockIdx.x * 256 + threadIdx.x;
-    if (c >= NB) return;
+    if (c >= NW) return;
     const Geom g = make_geom<Idx>(p);
     for (int64_t s = blockIdx.y; s < p.n; s += gridDim.y) {
         int64_t ca, ce;
         record_windows<K, Idx>(p, g, s, ca, ce);
         if (ce <= ca) {
             p.sum[s + p.ld * (int64_t)c] = 0;
+            if (P16) p.sum[s + p.ld * (int64_t)(c + NW)] = 0;
             continue;
         }
         const int64_t wf = ((ca >> kTileShift) - g.T0) / g.tpw;
         const int64_t wlast = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
         if (wf == wlast) continue;  // written directly by the count kernel
-        uint32_t acc = 0;
+        uint32_t lo = 0, hi = 0;
         for (int64_t w = wf; w <= wlast; ++w) {
-            if (p.slot_rec[2 * w] == s) acc += p.slab[(2 * w) * NB + c];
-            if (p.slot_rec[2 * w + 1] == s) acc += p.slab[(2 * w + 1) * NB + c];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (p.slot_rec[2 * w + q] == s) {
+                    const uint32_t v = p.slab[(2 * w + q) * NB + c];
+                    if (P16) {
+                        lo += v & 0xFFFFu;
+                        hi += v >> 16;
+                    } else {
+                        lo += v;
+                    }
+                }
+            }
         }
-        p.sum[s + p.ld * (int64_t)c] = (int32_t)acc;
+        p.sum[s + p.ld * (int64_t)c] = (int32_t)lo;
+        if (P16) p.sum[s + p.ld * (int64_t)(c + NW)] = (int32_t)hi;
     }
 }
 
@@ -812,9 +825,10 @@ int run_dense(const Request &q, hipStream_t st) {
         he = hipGetLastError();
         if (he != hipSuccess) return (int)he;
     }
-    const unsigned cb = (unsigned)((NB + 255) / 256);
-    hipLaunchKernelGGL((reduce_dense_kernel<K, Idx>), dim3(cb, (unsigned)std::min<int64_t>(q.n, kMaxGridY)), dim3(256),
-                       0, st, p);
+    constexpr int NWR = Cfg<K>::P16 ? NB / 2 : NB;  // slab words per slot
+    const unsigned cb = (unsigned)((NWR + 255) / 256);
+    hipLaunchKernelGGL((reduce_dense_kernel<K, Idx, Cfg<K>::P16>), dim3(cb, (unsigned)std::min<int64_t>(q.n, kMaxGridY)),
+                       dim3(256), 0, st, p);
     he = hipGetLastError();
     if (he != hipSuccess) return (int)he;
     if (Cfg<K>::P16) {

@@ -343,13 +343,27 @@ def test_gpu_counter_over_planned_shards(kmc, oracle, cuda, nshards):
 
 
 def test_count_multi_single_device(kmc, oracle, cuda):
-    """kmc_count_multi (host buffer -> shards -> RCCL all-reduce) on the box's one GPU."""
+    """kmc_count_multi (host buffer -> shards -> RCCL all-reduce) on the box's one GPU:
+    a first call creates the device set's communicator, later calls (other k, a
+    shard larger than one 32 MB pinned staging buffer) reuse it, and after
+    kmc_multi_release a call creates it again."""
     rng = np.random.default_rng(22)
     data, idx = random_records(rng, [200_000, 77_777, 3], 0.003, 0.003)
-    got, inv = kmc.count_multi(data, idx, 5, ndev=1, invalid=True)
-    exp, exp_inv = oracle.count_dense(data, idx, 5)
+    for k in (5, 8):
+        got, inv = kmc.count_multi(data, idx, k, ndev=1, invalid=True)
+        exp, exp_inv = oracle.count_dense(data, idx, k)
+        np.testing.assert_array_equal(got, exp)
+        np.testing.assert_array_equal(inv, exp_inv)
+    big, bidx = random_records(rng, [40_000_000, 30_000_001], 0.001, 0.0)  # 70 MB: three staging chunks
+    got, _ = kmc.count_multi(big, bidx, 4, ndev=1, devices=[0])
+    exp, _ = oracle.count_dense(big, bidx, 4)
     np.testing.assert_array_equal(got, exp)
-    np.testing.assert_array_equal(inv, exp_inv)
+    assert kmc.lib().kmc_multi_release() == 0
+    got, _ = kmc.count_multi(data, idx, 3, ndev=1)
+    exp, _ = oracle.count_dense(data, idx, 3)
+    np.testing.assert_array_equal(got, exp)
+    with pytest.raises(kmc.KmcError):  # one communicator rank per device
+        kmc.count_multi(data, idx, 3, ndev=2, devices=[0, 0])
 
 
 def test_synth_fill_range_matches_host(kmc, cuda):
