@@ -22,7 +22,8 @@
 //               workgroup's segment of each bucket (straight to the lists when a
 //               bucket is one list)
 //   K3b fine    one workgroup per coarse bucket of the records with more lists than
-//               buckets: the same staged sort by list, bucket -> its lists
+//               buckets: bucket -> its lists through per-list LDS rings flushed as
+//               whole 64-byte segments (Ring8; the radix path's R3 scheme)
 //   K4 count    two 512-thread workgroups per CU stride over the lists; a list
 //               (held in registers) is counted in an LDS table (4 096 slots,
 //               double hashing, 64-bit CAS claim, 32-bit add for repeats) in as
@@ -365,6 +366,148 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
     // thread reaches after this write-out
 }
 
+// Ring scatter of 8-byte entries (K3b, KMC_CANON_RING): the same scheme as
+// the radix path's R3 (kmc_radix.hip): a ring of RING = 16 384 / nbk entries per
+// bucket in LDS (128 KB in all), entries appended by one returning LDS add on the
+// bucket's word W[b] (ring half base << 16 | fill of the current 8-entry segment +
+// rank) and one ds_write_b64, whole 64-byte segments (8 entries) written to HBM
+// by the bucket's 1024 / nbk owner threads after a barrier, the other W buffer set
+// up by them (no third barrier).  Entries that do not fit the ring (a bucket
+// taking more than RING - 7 of a round's entries: skewed input) go straight to
+// their position in a cold path.  nbk = 2^lgb <= kMaxBk.
+constexpr int kRingEnt = 16384;  // 8-byte ring entries in LDS (128 KB)
+struct Ring8Lds {
+    unsigned long long ring[kRingEnt];
+    uint32_t W[2][kMaxBk];
+    unsigned long long gH[kMaxBk];
+    unsigned long long dummy[64];
+};
+
+struct Ring8 {
+    Ring8Lds *L;
+    uint64_t *dst;
+    int lgb;              // log2 buckets
+    int rlg;              // log2 ring entries per bucket
+    uint32_t par;
+    unsigned long long F, V;  // owner state of bucket tid >> (10 - lgb)
+
+    __device__ __forceinline__ uint32_t rmask() const { return (1u << rlg) - 1u; }
+    __device__ __forceinline__ uint32_t bucket_of_thread() const { return threadIdx.x >> (10 - lgb); }
+    __device__ __forceinline__ uint32_t member() const { return threadIdx.x & ((1u << (10 - lgb)) - 1u); }
+    __device__ __forceinline__ uint32_t rot(uint32_t b) const { return (8u * (b & 3u)) & rmask(); }
+    __device__ __forceinline__ uint32_t word(uint32_t b, unsigned long long f) const {
+        const uint32_t f0 = (uint32_t)f & 7u;
+        const uint32_t half = ((uint32_t)f - f0 + rot(b)) & rmask();
+        return (((b << rlg) + half) << 16) | f0;
+    }
+    // Start of a piece: bucket b's entries go to dst[f0 ...].  The caller
+    // synchronises before the first add.
+    __device__ __forceinline__ void init(Ring8Lds *lds, uint64_t *d, int lg_buckets, unsigned long long f0) {
+        L = lds;
+        dst = d;
+        lgb = lg_buckets;
+        rlg = 14 - lg_buckets;
+        par = 0;
+        F = f0;
+        V = f0;
+        if (member() == 0) {
+            const uint32_t b = bucket_of_thread();
+            L->W[0][b] = word(b, f0);
+            L->gH[b] = f0 & ~7ull;
+        }
+    }
+    // Phase A: entries val[j] (bit j of vm) to buckets bk[j].
+    template <int N>
+    __device__ __forceinline__ void add(const unsigned long long (&val)[N], const uint32_t (&bk)[N], uint32_t vm) {
+        const int lane = threadIdx.x & 63;
+        uint32_t *w = L->W[par];
+        uint32_t old[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            old[j] = 0u;
+            if ((vm >> j) & 1u)
+                old[j] = __hip_atomic_fetch_add(&w[bk[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        uint64_t ovf = 0u;
+        const uint32_t R = 1u << rlg;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const uint32_t lo = old[j] & 0xFFFFu, hi = old[j] >> 16;
+            const uint32_t idx = (hi & ~rmask()) | ((hi + lo) & rmask());
+            const bool v = (vm >> j) & 1u;
+            const bool ok = v && lo < R;
+            ovf |= __ballot(v && !ok);
+            unsigned long long *d = ok ? &L->ring[idx] : &L->dummy[lane];
+            *d = val[j];
+        }
+        if (__builtin_expect(ovf != 0u, 0)) {
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                const uint32_t lo = old[j] & 0xFFFFu;
+                if (((vm >> j) & 1u) && lo >= R) dst[L->gH[bk[j]] + lo] = val[j];
+            }
+        }
+    }
+    // Phase B (the caller brackets it with barriers).
+    __device__ __forceinline__ void flush() {
+        const uint32_t b = bucket_of_thread(), j = member(), tpb = 1u << (10 - lgb);
+        const uint32_t f0 = (uint32_t)F & 7u;
+        const uint32_t n = (L->W[par][b] & 0xFFFFu) - f0;
+        const unsigned long long F1 = F + n, H = F - f0;
+        const uint32_t R = 1u << rlg;
+        const unsigned long long top = F1 < H + R ? F1 : H + R;
+        const uint32_t nseg = (uint32_t)((top - H) >> 3);
+        const uint32_t rt = rot(b);
+        const uint4 *row = reinterpret_cast<const uint4 *>(&L->ring[b << rlg]);  // 2 entries per uint4
+        const uint32_t cm = (R >> 1) - 1u;  // chunk index mask
+        for (uint32_t i = j; i < nseg; i += tpb) {
+            const unsigned long long g0 = H + 8ull * i;
+            if (g0 >= V) {
+                const uint32_t c0 = (((uint32_t)g0 + rt) & rmask()) >> 1;
+                const uint32_t sh = ((b >> 2) + (i >> 2)) & 3u;  // rotated chunk order: spread the banks
+                const uint32_t q0 = sh, q1 = (sh + 1) & 3u, q2 = (sh + 2) & 3u, q3 = (sh + 3) & 3u;
+                const uint4 v0 = row[(c0 + q0) & cm], v1 = row[(c0 + q1) & cm];
+                const uint4 v2 = row[(c0 + q2) & cm], v3 = row[(c0 + q3) & cm];
+                uint4 *o = reinterpret_cast<uint4 *>(dst + g0);
+                o[q0] = v0;
+                o[q1] = v1;
+                o[q2] = v2;
+                o[q3] = v3;
+            } else {
+                for (uint32_t q = 0; q < 8; ++q)
+                    if (g0 + q >= V) dst[g0 + q] = L->ring[(b << rlg) + (((uint32_t)(g0 + q) + rt) & rmask())];
+            }
+        }
+        if (F1 > H + R) V = F1;  // [H + R, F1) went straight to dst
+        F = F1;
+        if (j == 0) {
+            L->W[par ^ 1u][b] = word(b, F1);
+            L->gH[b] = F1 & ~7ull;
+        }
+        par ^= 1u;
+    }
+    __device__ __forceinline__ void round_end() {
+        lds_barrier();
+        flush();
+        lds_barrier();
+    }
+    // End of a piece: the partial segment left in each ring, entry by entry.
+    __device__ __forceinline__ void finish() {
+        const uint32_t b = bucket_of_thread(), j = member(), tpb = 1u << (10 - lgb);
+        const unsigned long long H = F & ~7ull, lo = H > V ? H : V;
+        const uint32_t rt = rot(b);
+        for (unsigned long long g = lo + j; g < F; g += tpb)
+            dst[g] = L->ring[(b << rlg) + (((uint32_t)g + rt) & rmask())];
+    }
+};
+
+#ifndef KMC_CANON_RING
+#define KMC_CANON_RING 1
+#endif
+
+// (A ring version of K3a, as K3b's below, measured 10.5 -> 11.5 ms per C4 call: K3a
+// is bound by the key hashing of its input walk, and the rings' 8-entry rounds
+// need 4 barriers per 16 K windows against the staged sort's 3.)
 // K3a: every window's h at its coarse bucket's position (ent_c), or at its list
 // position (ent) for records whose buckets are single lists
 __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
@@ -401,6 +544,7 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
     });
 }
 
+
 // list boundaries: list (r, b) = off[cbase_r + b*nwg_r] .. off[cbase_r + (b+1)*nwg_r];
 // one thread per list (lbase is sorted: the record is a binary search)
 __global__ void canon_list_start_kernel(HParams p) {
@@ -418,6 +562,38 @@ __global__ void canon_list_start_kernel(HParams p) {
     p.list_start[l] = p.off[p.cbase[a] + (l - p.lbase[a]) * p.nwg[a]];
 }
 
+#if KMC_CANON_RING
+// K3b: one workgroup per coarse bucket of a record with several lists per bucket;
+// the bucket's entries (ent_c) to its lists (ent), 8 K entries per round through
+// the LDS rings (Ring8)
+__global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
+    __shared__ Ring8Lds R;
+    const int2 rc = p.fsplit[blockIdx.x];
+    const int lg = p.lg[rc.x], lgc = coarse_lg(lg);
+    const int lf = lg - lgc;  // log2 lists per coarse bucket (>= 1)
+    const int64_t F = (int64_t)1 << lf;
+    const int64_t lb = p.lbase[rc.x] + (int64_t)rc.y * F;
+    const uint64_t a0 = p.list_start[lb], a1 = p.list_start[lb + F];
+    Ring8 rg;
+    rg.init(&R, p.ent, lf, p.list_start[lb + (threadIdx.x >> (10 - lf))]);
+    __syncthreads();
+    for (uint64_t i0 = a0; i0 < a1; i0 += 8 * kWalkBlock) {
+        unsigned long long v[8];
+        uint32_t bk[8], vm = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
+            const unsigned long long x = i < a1 ? p.ent_c[i] : 0ull;
+            vm |= i < a1 ? 1u << j : 0u;
+            bk[j] = (uint32_t)(x >> (64 - lg)) & (uint32_t)(F - 1);
+            v[j] = list_value(x);
+        }
+        rg.add<8>(v, bk, vm);
+        rg.round_end();
+    }
+    rg.finish();
+}
+#else
 // K3b: one workgroup per coarse bucket of a record with several lists per bucket;
 // the bucket's entries (ent_c) to its lists (ent)
 __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
@@ -448,6 +624,8 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
         par ^= 1;
     }
 }
+
+#endif
 
 // K4: lists counted in an LDS table, workgroups striding over the lists.  Its
 // barriers are LDS-only (lds_barrier): __syncthreads would also wait for the pair

@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/c4r && mkdir -p $O && rm -rf $O/*
 timeout -k 10 600 python -u -m pytest tests/test_hash_gpu.py -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log; if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED" $O/tests.log | head -20; exit $rc; fi
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/cb -o cb -- python3 scripts/cbench.py --configs ${CFGS:-c4,c4r} --iters 3 > $O/cb.log 2>&1 || { tail -20 $O/cb.log; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/cb -o cb -- python3 scripts/cbench.py --configs ${CFGS:-c4,c4r} --iters 3 --cpu-sample-c4 0 > $O/cb.log 2>&1 || { tail -20 $O/cb.log; exit 1; }
 grep '^{' $O/cb.log
 python3 - <<'PY'
 import csv, glob
