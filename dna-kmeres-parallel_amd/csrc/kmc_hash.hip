@@ -33,7 +33,9 @@
 //               wave claimed are written (claim order) to the list's segment and
 //               cleared
 //   K5 place    exclusive scan of the distinct counts; each list's pairs are copied
-//               to their final place; records are contiguous runs of lists
+//               to their final place; records are contiguous runs of lists (K4
+//               writes 8 bytes per pair: counts 1..3 in the key's two spare top
+//               bits, larger ones in a side array)
 // Bytes per window: the input twice (K1, K3a), an 8-byte h written and read twice
 // (K3a -> K3b -> K4), 12 bytes of pairs written, read and written again.
 #include <hip/hip_runtime.h>
@@ -889,8 +891,11 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 if (c == 0xFFFFFFF0u)
 #endif
                 {
-                    p.pk[out + before + i] = unmix64(h);
-                    p.pc[out + before + i] = c + 1u;
+                    // keys use at most 62 bits (k <= 31): occurrences 1..3 ride in the
+                    // top two bits, larger counts escape to pc (K5 reads it only then)
+                    const unsigned long long tag = c < 3u ? c : 3u;
+                    p.pk[out + before + i] = unmix64(h) | (tag << 62);
+                    if (c >= 3u) p.pc[out + before + i] = c + 1u;
                 }
             }
             out += total;
@@ -931,8 +936,10 @@ __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
     const int64_t l = blockIdx.x;
     const uint64_t src = p.list_start[l], dst = p.dist_off[l], m = p.ndist[l];
     for (uint64_t i = threadIdx.x; i < m; i += 256) {
-        p.out_keys[dst + i] = p.pk[src + i];
-        p.out_counts[dst + i] = p.pc[src + i];
+        const uint64_t x = p.pk[src + i];
+        const uint32_t tag = (uint32_t)(x >> 62);
+        p.out_keys[dst + i] = x & 0x3FFFFFFFFFFFFFFFull;
+        p.out_counts[dst + i] = tag < 3u ? tag + 1u : p.pc[src + i];
     }
 }
 
