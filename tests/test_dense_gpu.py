@@ -450,3 +450,25 @@ def test_many_short_records(kmc, oracle, cuda, k, n):
         assert int(inv[s]) == int(exp_inv[0])
     del out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k", [9, 13])
+def test_radix_sum_ld_column_block(kmc, oracle, cuda, k):
+    """k >= 9 into columns [off, off+n) of a wider matrix (ld > n: the R5 tile
+    transpose; ld == n takes the contiguous one), 25 records (not a multiple of
+    R5's 16-record tiles), other columns untouched."""
+    import torch
+    rng = np.random.default_rng(90 + k)
+    data, idx = random_records(rng, list(rng.integers(0, 40_000, size=25)), 0.002, 0.0)
+    n, ld, off = idx.size - 1, 31, 3
+    big = torch.full((1 << (2 * k), ld), -1, dtype=torch.int32, device=cuda)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    kmc.count_dense_ex(kmc.dense_args(d, di, k, big.view(-1)[off:], ld=ld))
+    torch.cuda.synchronize()
+    exp, _ = oracle.count_dense(data, idx, k)
+    got = big.cpu().numpy()
+    np.testing.assert_array_equal(got[:, off:off + n], exp)
+    assert (got[:, :off] == -1).all() and (got[:, off + n:] == -1).all()
+    del big
+    out, _ = run_dense(kmc, cuda, data, idx, k)  # ld == n, 25 records
+    np.testing.assert_array_equal(out, exp)
