@@ -36,6 +36,9 @@
 #define KMC_RSCAT_PF 2
 #endif
 // tiles per wave in one R3 ring round (more: fewer barriers, more ring overflows)
+#ifndef KMC_RING_PROF
+#define KMC_RING_PROF 0  // diagnostic: per-phase shader-clock cycles of workgroup 0 (printf)
+#endif
 #ifndef KMC_RING_RT
 #define KMC_RING_RT 1
 #endif
@@ -152,29 +155,33 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
 // RING uint16 entries per bucket in LDS; whenever a 64-byte-aligned segment of the
 // list (32 entries) is complete in a ring it is written out whole.  Each round is
 // one tile per wave (16 K windows):
-//   A  per valid window one returning LDS add on its bucket's word W[b], which
-//      holds (halfword address of the bucket's current ring half) << 16 | (fill
-//      of the ring's current 32-entry segment + windows ranked so far): the
-//      returned value gives the entry's LDS address in three VALU ops and whether
-//      it fits (low half < RING: the ring holds at most 31 carried entries).  The
-//      ds_write_b16 is unconditional (windows that are invalid or do not fit write
-//      a per-lane dummy word); entries that do not fit go straight to their list
-//      position in a cold path (uncoalesced 2-byte stores; skewed input only);
+//   A  per valid window one returning LDS add of 2 on its bucket's word W[b], which
+//      holds (halfword index of the bucket's ring | its swizzle) << 16 | 2 * (fill
+//      of the ring: the carried partial segment + windows ranked so far).  The
+//      returned value o gives the entry's LDS byte address in two VALU ops,
+//      (o >> 15) ^ (o & (2 RING - 1)), and whether it fits in one 16-bit compare
+//      (low half < 2 RING).  The ds_write_b16 is unconditional (windows that are
+//      invalid or do not fit write a per-lane dummy word); entries that do not fit
+//      go straight to their list position in a cold path (uncoalesced 2-byte
+//      stores; skewed input only);
 //   B  after a barrier, the TPB threads of bucket b (all keeping the bucket's state
 //      in registers: F = list index of its next entry, V = first index still to be
 //      written from the ring) write its complete segments (4 ds_read_b128 + 4
-//      global 16-byte stores each), and thread 0 of the group sets up the other W
+//      global 16-byte stores each), thread 0 of the group moves the partial last
+//      segment to the ring's start (at most 4 b128 copies) and sets up the other W
 //      buffer (W alternates per round, so the reset needs no third barrier).
-// List position g of bucket b lives in ring slot (g + rot(b)) mod RING: the
-// per-bucket rotation (a multiple of 8 slots) spreads the phase-B 16-byte reads of
-// neighbouring buckets over the banks, and the TPB threads of one bucket read
+// Between flushes list position g of bucket b lives in ring slot (g - H) ^ swz(b),
+// H = the start of the round's first (partial) segment: the ring never wraps, and
+// the per-bucket XOR swizzle (a multiple of 8 slots) spreads the phase-B 16-byte
+// reads of neighbouring buckets over the banks; the TPB threads of one bucket read
 // their segments' chunks in rotated order for the same reason.  Positions below V
 // (before this workgroup's segment of the list, or already stored directly) are
 // never written from the ring.  At the end of a piece the partial segment left in
 // a ring is written entry by entry.
-// Per window: 1 returning LDS atomic + 1 ds_write_b16 (the staged counting sort
-// this replaces needed 4 LDS accesses, a block scan and 5 barriers per round),
-// and every global write is a whole 64-byte segment except at list ends.
+// Per window: 1 returning LDS atomic + 1 ds_write_b16 + 4 VALU ops (the staged
+// counting sort this replaces needed 4 LDS accesses, a block scan and 5 barriers
+// per round), and every global write is a whole 64-byte segment except at list
+// ends.
 template <int K>
 struct RingGeom {
     static constexpr int LOW = low_bits(K);
@@ -182,139 +189,210 @@ struct RingGeom {
     static constexpr int BLOCK = 1024;
     static constexpr int TPB = BLOCK / NBK;     // threads per bucket in phase B
     static constexpr int RING = 65536 / NBK;    // entries per bucket ring (128 KB in all)
-    static constexpr int CH = RING / 8;         // 16-byte chunks per ring
     static_assert(NBK <= BLOCK && RING >= 64 && (RING & (RING - 1)) == 0, "ring geometry");
+    // the fill (in bytes) of one round stays below 2^16: it cannot carry into the ring field
+    static_assert(2 * (BLOCK * 16 * KMC_RING_RT + 32) < 65536, "one tile per wave per round");
 };
 
-template <int K>
-__device__ __forceinline__ uint32_t ring_rot(uint32_t b) {
-    return ((b >> 1) & 7u) * 8u;
+// o[t] = x of lane t of this lane's quad (DPP quad_perm broadcasts)
+__device__ __forceinline__ void quad_bcast4(uint32_t x, uint32_t *o) {
+    o[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x00, 0xF, 0xF, false);
+    o[1] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x55, 0xF, 0xF, false);
+    o[2] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xAA, 0xF, 0xF, false);
+    o[3] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xFF, 0xF, 0xF, false);
 }
 
-// W word of bucket b for a round that starts at list index F
+// slot swizzle of bucket b (XOR mask, a multiple of 8 slots below 64)
+__device__ __forceinline__ uint32_t ring_swz(uint32_t b) { return ((b >> 1) & 7u) * 8u; }
+
+// W word of bucket b for a round whose first entry goes to ring slot f0 (< 32)
 template <int K>
-__device__ __forceinline__ uint32_t ring_word(uint32_t b, unsigned long long F) {
-    using RG = RingGeom<K>;
-    const uint32_t f0 = (uint32_t)F & 31u;
-    const uint32_t half = ((uint32_t)F - f0 + ring_rot<K>(b)) & (uint32_t)(RG::RING - 1);
-    return ((b * (uint32_t)RG::RING + half) << 16) | f0;
+__device__ __forceinline__ uint32_t ring_word(uint32_t b, uint32_t f0) {
+    return ((b * (uint32_t)RingGeom<K>::RING | ring_swz(b)) << 16) | (f0 << 1);
 }
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
 template <int K>
 struct RRingOp {
     using RG = RingGeom<K>;
     uint16_t *ring;        // LDS, NBK * RING entries
     uint32_t *W;           // LDS, [2][NBK]
-    unsigned long long *gH;  // LDS, [NBK]: floor32(F) of every bucket at the start of the round
+    unsigned long long *gH;  // LDS, [NBK]: list index of every bucket's ring slot 0 this round
     uint16_t *dummy;       // LDS, 2 halfwords per lane
     uint16_t *ent;
     int tid, lane;
     uint32_t par;          // W buffer of this round
-    // phase-B state of bucket tid / TPB (replicated over its TPB threads)
-    unsigned long long F, V;
+    // phase-B state of bucket tid / TPB (replicated over its TPB threads), list
+    // indices relative to P0 = this piece's first list index rounded down to 32:
+    // f = next entry, v = first entry still to be written from the ring
+    unsigned long long P0;
+    uint32_t f, v;
+    int held = 0;          // tiles of this round taken (workgroup-uniform)
+#if KMC_RING_PROF
+    // diagnostic: shader-clock cycles per phase, summed over this wave's rounds
+    unsigned long long t_last = 0, t_sc = 0, t_b1 = 0, t_fl = 0, t_b2 = 0, rounds = 0;
+#endif
 
     __device__ void before_tile() {}
 
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t l, uint32_t h, uint32_t Wm) {
-        uint32_t *w = W + par * RG::NBK;
-        uint32_t old[16];
+        const uint32_t wb = (uint32_t)(uintptr_t)(W + par * RG::NBK);  // LDS byte address, 4 NBK-aligned
+        uint32_t c[16], old[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) c[j] = __builtin_amdgcn_alignbit(h, l, 2 * j);  // low 2k bits: the window
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);  // low 2k bits: the window
+            // 4 * bucket of window j = bits [2j + LOW, 2j + 2k) of the tile at bit 2:
+            // for even LOW that is in the window (LOW - 2) / 2 bases on when there is
+            // one in this tile; v_bitop3 (x & mask) | wb keeps it one op (the ORed
+            // base has zero low bits)
+            constexpr int SH = RG::LOW - 2;
+            const int sh = 2 * j + SH;
+            uint32_t x;
+            if ((SH & 1) == 0 && j + SH / 2 < 16) x = c[j + SH / 2];
+            else x = sh < 32 ? __builtin_amdgcn_alignbit(h, l, sh) : h >> (sh - 32);
+            const uint32_t wa = __builtin_amdgcn_bitop3_b32(x, (uint32_t)(4 * RG::NBK - 4), wb, 0xEA);
             old[j] = 0u;
             if (!MASKED || ((Wm >> j) & 1u))
-                old[j] = __hip_atomic_fetch_add(&w[(c >> RG::LOW) & (RG::NBK - 1)], 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+                old[j] = __hip_atomic_fetch_add((__attribute__((address_space(3))) uint32_t *)(uintptr_t)wa, 2u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        uint32_t any = 0u;  // OR of the returned words: low half >= RING iff some entry did not fit
+        uint32_t any = 0u;  // OR of the returned words: low half >= 2 RING iff some entry did not fit
+        // 2 RING, opaque to the compiler so the fit test stays one 16-bit compare
+        uint32_t cap2;
+        asm("s_mov_b32 %0, %1" : "=s"(cap2) : "i"(2 * RG::RING));
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);
-            const uint32_t hi = old[j] >> 16;
-            // halfword index: the ring half's base (hi) with the in-ring offset
-            // (hi + lo) mod RING inserted (one v_bfi); hi + old has the same low bits
-            const uint32_t hw = __builtin_amdgcn_ubfe(hi + old[j], 0, 31) & (uint32_t)(RG::RING - 1);
-            const uint32_t idx = hw | (hi & ~(uint32_t)(RG::RING - 1));
-            bool ok = (old[j] & 0xFFFFu) < (uint32_t)RG::RING;
+            const uint32_t o = old[j];
+            // byte offset: 2 * (b RING | swz) with the fill XORed into its low bits
+            const uint32_t off = (o >> 15) ^ (o & (uint32_t)(2 * RG::RING - 1));
+            bool ok = (uint16_t)o < (uint16_t)cap2;
             if (MASKED) ok = ok && ((Wm >> j) & 1u);
-            uint16_t *dst = ok ? ring + idx : dummy + 2 * lane;
+            uint16_t *dst = ok ? reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(ring) + off)
+                               : dummy + 2 * lane;
             // the entry: the low LOW bits (ds_write_b16 drops the rest when LOW = 16)
-            *dst = (uint16_t)(RG::LOW == 16 ? c : c & ((1u << RG::LOW) - 1u));
-            any |= old[j];
+            *dst = (uint16_t)(RG::LOW == 16 ? c[j] : c[j] & ((1u << RG::LOW) - 1u));
+            any |= o;
         }
-        if (__builtin_expect(__any((any & 0xFFFFu) >= (uint32_t)RG::RING), 0)) {
+        if (__builtin_expect(__any((any & 0xFFFFu) >= (uint32_t)(2 * RG::RING)), 0)) {
             // ring full: straight to the list (skewed input)
             for (int j = 0; j < 16; ++j) {
-                const uint32_t c = __builtin_amdgcn_alignbit(h, l, 2 * j);
-                const uint32_t lo = old[j] & 0xFFFFu;
+                const uint32_t lo = (old[j] & 0xFFFFu) >> 1;
                 if ((!MASKED || ((Wm >> j) & 1u)) && lo >= (uint32_t)RG::RING)
-                    ent[gH[(c >> RG::LOW) & (RG::NBK - 1)] + lo] = (uint16_t)(c & ((1u << RG::LOW) - 1u));
+                    ent[gH[(c[j] >> RG::LOW) & (RG::NBK - 1)] + lo] = (uint16_t)(c[j] & ((1u << RG::LOW) - 1u));
             }
         }
     }
 
-    // entry at list position g of bucket b, from the ring
-    __device__ __forceinline__ uint16_t ring_entry(uint32_t b, unsigned long long g) const {
-        return ring[b * RG::RING + (((uint32_t)g + ring_rot<K>(b)) & (RG::RING - 1))];
+    // entry at relative list index g of bucket b, from the ring (h: ring slot 0's index)
+    __device__ __forceinline__ uint16_t ring_entry(uint32_t b, uint32_t h, uint32_t g) const {
+        return ring[b * RG::RING + ((g - h) ^ ring_swz(b))];
     }
 
-    // phase B for this thread's bucket; the caller brackets it with barriers
+    // start of a piece: list (s, b)'s segment of this workgroup begins at F
+    __device__ __forceinline__ void begin(uint32_t b, unsigned long long F, bool owner) {
+        P0 = F & ~31ull;
+        f = v = (uint32_t)(F - P0);
+        if (owner) {
+            W[b] = ring_word<K>(b, f);
+            gH[b] = P0;
+        }
+    }
+
+    // phase B for this thread's bucket; the caller brackets it with barriers.
+    // Complete segments leave as whole 64-byte stores by lane quads (one lane per
+    // segment issues 64 scattered 16-byte pieces per store, ~2x slower in HBM:
+    // scripts/write_microbench.hip): in pass t every quad stores the segment of
+    // its lane t, whose ring address and list index / 32 reach the quad by DPP
+    // broadcasts (VALU, no LDS round trip).  All bookkeeping is 32-bit.
     __device__ __forceinline__ void flush() {
         const uint32_t b = (uint32_t)tid / RG::TPB, j = (uint32_t)tid % RG::TPB;
-        const uint32_t f0 = (uint32_t)F & 31u;
-        const uint32_t n = (W[par * RG::NBK + b] & 0xFFFFu) - f0;
-        const unsigned long long F1 = F + n;
-        const unsigned long long H = F - f0;
-        const unsigned long long top = F1 < H + RG::RING ? F1 : H + RG::RING;
-        const uint32_t nseg = (uint32_t)((top - H) >> 5);
-        const uint32_t rot = ring_rot<K>(b);
-        const uint4 *row = reinterpret_cast<const uint4 *>(ring + b * RG::RING);
-        for (uint32_t i = j; i < nseg; i += RG::TPB) {
-            const unsigned long long g0 = H + 32ull * i;
-            if (g0 >= V) {
-                const uint32_t c0 = (((uint32_t)g0 + rot) & (RG::RING - 1)) >> 3;  // first 16-byte chunk
-                const uint32_t sh = (i >> 2) & 3u;  // rotated chunk order: TPB readers of one ring
-                uint4 *dst = reinterpret_cast<uint4 *>(ent + g0);
-                const uint32_t q0 = sh, q1 = (sh + 1) & 3u, q2 = (sh + 2) & 3u, q3 = (sh + 3) & 3u;
-                const uint4 v0 = row[(c0 + q0) & (RG::CH - 1)];
-                const uint4 v1 = row[(c0 + q1) & (RG::CH - 1)];
-                const uint4 v2 = row[(c0 + q2) & (RG::CH - 1)];
-                const uint4 v3 = row[(c0 + q3) & (RG::CH - 1)];
-                dst[q0] = v0;
-                dst[q1] = v1;
-                dst[q2] = v2;
-                dst[q3] = v3;
-            } else {
-                for (uint32_t q = 0; q < 32; ++q)
-                    if (g0 + q >= V) ent[g0 + q] = ring_entry(b, g0 + q);
-            }
+        const uint32_t h = f & ~31u;  // ring slot 0
+        const uint32_t fill = (W[par * RG::NBK + b] & 0xFFFFu) >> 1;  // slots used (or wanted) this round
+        const uint32_t f1 = h + fill;
+        const uint32_t nseg = (fill < (uint32_t)RG::RING ? fill : (uint32_t)RG::RING) >> 5;
+        const uint32_t x8 = ring_swz(b) >> 3;  // the swizzle in 16-byte chunks
+        uint4 *row = reinterpret_cast<uint4 *>(ring + b * RG::RING);
+        // the partial last segment moves to the ring's start at the end (after
+        // this wave's reads of segment 0; no other thread reads segments 0 or
+        // nseg); its chunks are read now, their latency hidden
+        const uint32_t nq = (fill <= (uint32_t)RG::RING && j == 0 && nseg > 0) ? ((fill & 31u) + 7u) >> 3 : 0u;
+        uint4 tl0, tl1, tl2, tl3;
+        if (nq > 0) tl0 = row[(4 * nseg + 0) ^ x8];
+        if (nq > 1) tl1 = row[(4 * nseg + 1) ^ x8];
+        if (nq > 2) tl2 = row[(4 * nseg + 2) ^ x8];
+        if (nq > 3) tl3 = row[(4 * nseg + 3) ^ x8];
+        uint32_t i0 = j;
+        if (h < v && j == 0 && nseg > 0) {  // segment 0 partly before v (piece start, after an overflow)
+            for (uint32_t q = 0; q < 32; ++q)
+                if (h + q >= v) ent[P0 + h + q] = ring_entry(b, h, h + q);
+            i0 = j + RG::TPB;
         }
-        if (F1 > H + RG::RING) V = F1;  // [H + RING, F1) went straight to the list
-        F = F1;
+        const uint32_t q = (uint32_t)lane & 3u;
+        const uint32_t rowb = (uint32_t)(uintptr_t)row;                      // LDS byte address of the ring
+        const uint32_t gs = (uint32_t)((P0 + h) >> 5);                        // list index / 32 of slot 0
+        for (uint32_t i = i0; __any(i < nseg); i += RG::TPB) {  // mostly once: two segments are rare
+            // bit 2: a segment to store; bits 0-1: the chunk swizzle
+            const uint32_t A = (rowb + 64u * (i ^ (x8 >> 2))) | (x8 & 3u) | (i < nseg ? 4u : 0u);
+            uint32_t a[4], g[4];
+            quad_bcast4(A, a);
+            quad_bcast4(gs + i, g);
+            u32x4 val[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (a[t] & 4u) val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (a[t] & 4u) reinterpret_cast<u32x4 *>(ent + 32ull * g[t])[q] = val[t];
+        }
+        if (fill > (uint32_t)RG::RING) {
+            v = f1;  // [h + RING, f1) went straight to the list
+        } else {     // the partial last segment to the ring's start
+            if (nq > 0) row[0 ^ x8] = tl0;
+            if (nq > 1) row[1 ^ x8] = tl1;
+            if (nq > 2) row[2 ^ x8] = tl2;
+            if (nq > 3) row[3 ^ x8] = tl3;
+        }
+        f = f1;
         if (j == 0) {
-            W[(par ^ 1u) * RG::NBK + b] = ring_word<K>(b, F1);
-            gH[b] = F1 & ~31ull;
+            W[(par ^ 1u) * RG::NBK + b] = ring_word<K>(b, f1 & 31u);
+            gH[b] = P0 + (f1 & ~31u);
         }
         par ^= 1u;
     }
 
-    int held = 0;  // tiles of this round taken (workgroup-uniform)
-
     __device__ void after_iter(int64_t i, int64_t per, bool) {
         if (++held < KMC_RING_RT && i + 1 < per) return;
         held = 0;
+#if KMC_RING_PROF
+        const unsigned long long ta = __builtin_readcyclecounter();
+        if (t_last) t_sc += ta - t_last;
+#endif
         lds_barrier();  // every window of the round is ranked and in its ring
+#if KMC_RING_PROF
+        const unsigned long long tb = __builtin_readcyclecounter();
+#endif
         flush();
+#if KMC_RING_PROF
+        const unsigned long long tc = __builtin_readcyclecounter();
+#endif
         lds_barrier();  // rings read, W set up: the next round may write
+#if KMC_RING_PROF
+        const unsigned long long td = __builtin_readcyclecounter();
+        if (t_last) { t_b1 += tb - ta; t_fl += tc - tb; t_b2 += td - tc; ++rounds; }
+        t_last = td;
+#endif
     }
 
     // end of a piece: the partial segment left in the ring, entry by entry
     __device__ __forceinline__ void finish() {
         const uint32_t b = (uint32_t)tid / RG::TPB, j = (uint32_t)tid % RG::TPB;
-        const unsigned long long H = F & ~31ull;
-        const unsigned long long lo = H > V ? H : V;
-        for (unsigned long long g = lo + j; g < F; g += RG::TPB) ent[g] = ring_entry(b, g);
+        const uint32_t h = f & ~31u;
+        const uint32_t lo = h > v ? h : v;
+        for (uint32_t g = lo + j; g < f; g += RG::TPB) ent[P0 + g] = ring_entry(b, h, g);
     }
 };
 
@@ -358,12 +436,7 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         op.tid = tid;
         op.lane = lane;
         op.par = 0;
-        op.F = p.off[((s * RG::NBK) + b) * p.G + w];  // this workgroup's segment of list (s, b)
-        op.V = op.F;
-        if ((uint32_t)tid % RG::TPB == 0) {
-            s_W[b] = ring_word<K>(b, op.F);
-            s_gH[b] = op.F & ~31ull;
-        }
+        op.begin(b, p.off[((s * RG::NBK) + b) * p.G + w], (uint32_t)tid % RG::TPB == 0);  // this workgroup's segment of list (s, b)
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
         const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
@@ -373,6 +446,12 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         op.finish();
         __syncthreads();
+#if KMC_RING_PROF
+        if (w == 0 && lane == 0 && op.rounds > 0)
+            printf("ring_prof k=%d wave=%d rec=%lld rounds=%llu scatter=%.0f bar1=%.0f flush=%.0f bar2=%.0f cyc/round\n", K,
+                   wave, (long long)s, op.rounds, (double)op.t_sc / op.rounds, (double)op.t_b1 / op.rounds,
+                   (double)op.t_fl / op.rounds, (double)op.t_b2 / op.rounds);
+#endif
     }
 }
 

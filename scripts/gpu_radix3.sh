@@ -13,7 +13,15 @@ for r in csv.DictReader(open(f)):
     if "at::" in n or "rocprim" in n or "rocclr" in n: continue
     print("%-60s %5s %10.3f ms avg %10.3f max" % (n[:60], r["Calls"], float(r["AverageNs"]) / 1e6, float(r["MaxNs"]) / 1e6))
 PY
-for f in dna-kmeres-parallel_amd/lib/variants/*.so; do [ -e "$f" ] || continue
-  echo "== $f"; KMC_LIB=$PWD/$f timeout -k 10 300 python scripts/cbench.py --configs c3 --iters 5 --cpu-sample-c3 0 > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 1; }
-  grep '^{' $O/var.log | cut -c1-220
+for f in dna-kmeres-parallel_amd/lib/variants/${VAR_GLOB:-*}.so; do [ -e "$f" ] || continue
+  v=$(basename $f .so); echo "== $v"
+  KMC_LIB=$PWD/$f timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$v -o cb -- python3 scripts/cbench.py --configs c3 --iters 5 --cpu-sample-c3 0 ${VARARGS:-} > $O/var.log 2>&1 || { tail -5 $O/var.log; exit 1; }
+  grep '^{' $O/var.log | cut -c1-150
+  python3 - $O/$v <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    n = r["Name"].replace("(anonymous namespace)::", "").replace("kmc::", "")
+    if "radix" in n: print("   %-50s %10.3f ms avg" % (n[:50], float(r["AverageNs"]) / 1e6))
+PY
 done
