@@ -319,12 +319,13 @@ struct RRingOp {
         // the partial last segment moves to the ring's start at the end (after
         // this wave's reads of segment 0; no other thread reads segments 0 or
         // nseg); its chunks are read now, their latency hidden
+        // (unconditional reads, inside the bucket's own ring: predicated ones
+        // would each wait for the last)
         const uint32_t nq = (fill <= (uint32_t)RG::RING && j == 0 && nseg > 0) ? ((fill & 31u) + 7u) >> 3 : 0u;
-        uint4 tl0, tl1, tl2, tl3;
-        if (nq > 0) tl0 = row[(4 * nseg + 0) ^ x8];
-        if (nq > 1) tl1 = row[(4 * nseg + 1) ^ x8];
-        if (nq > 2) tl2 = row[(4 * nseg + 2) ^ x8];
-        if (nq > 3) tl3 = row[(4 * nseg + 3) ^ x8];
+        const uint4 tl0 = row[((4 * nseg + 0) ^ x8) & (RG::RING / 8 - 1)];
+        const uint4 tl1 = row[((4 * nseg + 1) ^ x8) & (RG::RING / 8 - 1)];
+        const uint4 tl2 = row[((4 * nseg + 2) ^ x8) & (RG::RING / 8 - 1)];
+        const uint4 tl3 = row[((4 * nseg + 3) ^ x8) & (RG::RING / 8 - 1)];
         uint32_t i0 = j;
         if (h < v && j == 0 && nseg > 0) {  // segment 0 partly before v (piece start, after an overflow)
             for (uint32_t q = 0; q < 32; ++q)
@@ -340,10 +341,9 @@ struct RRingOp {
             uint32_t a[4], g[4];
             quad_bcast4(A, a);
             quad_bcast4(gs + i, g);
-            u32x4 val[4];
+            u32x4 val[4];  // (a quad without a segment reads a chunk of its own ring harmlessly)
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (a[t] & 4u) val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
+            for (int t = 0; t < 4; ++t) val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (a[t] & 4u) reinterpret_cast<u32x4 *>(ent + 32ull * g[t])[q] = val[t];
