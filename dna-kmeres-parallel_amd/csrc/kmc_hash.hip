@@ -88,7 +88,10 @@ constexpr int kWaves4 = kCountBlock / 64;
 #define KMC_CANON_STAGE 320
 #endif
 constexpr int kStage = KMC_CANON_STAGE;                // K4 per-wave keys staged for one probe loop
-constexpr int kClaimW = 320;                 // K4 per-wave claims per pass (2-byte slot ids)
+#ifndef KMC_CANON_CLAIMW
+#define KMC_CANON_CLAIMW 320
+#endif
+constexpr int kClaimW = KMC_CANON_CLAIMW;      // K4 per-wave claims per pass (2-byte slot ids)
 constexpr uint32_t kMaxInitPasses = 16;
 constexpr int kPassTop = 64 - kMaxLg;          // pass bits [kPassTop - log2 P, kPassTop), below the list bits
 constexpr uint32_t kMaxPasses = 1u << (kPassTop - 32);
@@ -219,15 +222,24 @@ __device__ __forceinline__ uint32_t chunk_keys(const HParams &p, int64_t q, int6
     const uint64_t lo64 = (uint64_t)cd[0] | ((uint64_t)cd[1] << 32);
     const uint64_t badm = (uint64_t)bd[0] | ((uint64_t)bd[1] << 16) | ((uint64_t)bd[2] << 32);
     const int64_t last = std::min<int64_t>(pe, rend - k);  // window starts < last
-    uint32_t vm = 0u;
+    // window starts [ps, last) of this chunk as a mask (32-bit compares: the
+    // chunk's offsets are 0..15)
+    const int64_t lo_j = ps - q, hi_j = last - q;
+    const uint32_t lo_m = lo_j <= 0 ? 0xFFFFu : (lo_j >= 16 ? 0u : (0xFFFFu << lo_j) & 0xFFFFu);
+    const uint32_t hi_m = hi_j >= 16 ? 0xFFFFu : (hi_j <= 0 ? 0u : (1u << hi_j) - 1u);
+    uint32_t vm = lo_m & hi_m;
+    // the MSB-first key of window 0 by bit reversal, then rolled one base per
+    // window: base j + k - 1 enters at the low end, read from t = the chunk's
+    // codes from base k - 1 on (2 <= 2(k - 1) <= 60)
+    uint64_t fw = reverse_groups(lo64 & kmask, k);
+    const int sk = 2 * (k - 1);
+    const uint64_t t = sk == 0 ? lo64 : (lo64 >> sk) | ((uint64_t)cd[2] << (64 - sk));
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const int64_t pos = q + j;
-        const bool v = pos >= ps && pos < last && !((badm >> j) & wmask);
+        if ((badm >> j) & wmask) vm &= ~(1u << j);
         const uint64_t le = (j == 0 ? lo64 : ((lo64 >> (2 * j)) | ((uint64_t)cd[2] << (64 - 2 * j)))) & kmask;
-        const uint64_t fw = reverse_groups(le, k);
+        if (j > 0) fw = ((fw << 2) | ((t >> (2 * j)) & 3u)) & kmask;
         h[j] = part_of(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
-        vm |= v ? 1u << j : 0u;
     }
     return vm;
 }
@@ -662,7 +674,16 @@ struct K4Lds {
 };
 
 #ifdef KMC_CANON_PROF
-__device__ unsigned long long g_prof2[4];  // probe rounds, staged keys, probe loops
+__device__ unsigned long long g_prof2[4];  // probe rounds, staged keys, probe loops, CAS-wait cycles
+// per-wave counters in registers, added to g_prof2 once per wave at the end
+struct ProbeProf {
+    unsigned long long rounds = 0, keys = 0, loops = 0, cas = 0;
+};
+#define PROF_PARAM , ProbeProf &pp
+#define PROF_PASS , pp
+#else
+#define PROF_PARAM
+#define PROF_PASS
 #endif
 // LDS byte offset of a __shared__ object
 template <class T>
@@ -688,7 +709,7 @@ __device__ __forceinline__ unsigned long long lds_cas64(uint32_t off, unsigned l
 // raises *ovf and stops (the pass is redone split in two), which also bounds the
 // table's load below one: no probe chain can wrap.
 __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint32_t cap, uint32_t *ovf,
-                                             uint32_t &ncl) {
+                                             uint32_t &ncl PROF_PARAM) {
 #ifdef KMC_CANON_PROF
     uint32_t rounds = 0;
 #endif
@@ -716,7 +737,13 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
 #ifdef KMC_CANON_PROF
         ++rounds;
 #endif
+#ifdef KMC_CANON_PROF
+        const unsigned long long tcas = __builtin_amdgcn_s_memtime();
+#endif
         const unsigned long long cur = lds_cas64(busy ? tk0 + 8u * s : dummy, kEmptyH, h);
+#ifdef KMC_CANON_PROF
+        pp.cas += __builtin_amdgcn_s_memtime() - tcas;
+#endif
         const bool claimed = busy && cur == kEmptyH;  // first occurrence (tc holds occurrences - 1)
         const bool dup = busy && cur == h;
         if (__ballot(dup)) {
@@ -734,11 +761,9 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
         }
     }
 #ifdef KMC_CANON_PROF
-    if (lane == 0) {
-        atomicAdd(&g_prof2[0], (unsigned long long)rounds);
-        atomicAdd(&g_prof2[1], (unsigned long long)nq);
-        atomicAdd(&g_prof2[2], 1ull);
-    }
+    pp.rounds += rounds;
+    pp.keys += nq;
+    pp.loops += 1;
 #endif
 }
 
@@ -752,7 +777,7 @@ __device__ __forceinline__ uint32_t pass_of(unsigned long long h, uint32_t P) {
 // The wave's keys of pass q / P, staged in its LDS queue and probed; a queue that
 // fills up (repeats beyond the pass target) is probed and refilled.
 __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes], uint32_t q, uint32_t P, K4Lds &L,
-                                            int wv, uint32_t cap, uint32_t *ovf, uint32_t &ncl) {
+                                            int wv, uint32_t cap, uint32_t *ovf, uint32_t &ncl PROF_PARAM) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long *qk = L.qk[wv];
@@ -770,7 +795,7 @@ __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes]
                 next = j + 1;
             }
         }
-        if (nq) probe_staged(L, wv, nq, cap, ovf, ncl);
+        if (nq) probe_staged(L, wv, nq, cap, ovf, ncl PROF_PASS);
     } while (next < kRes && ncl <= cap);
 }
 
@@ -788,6 +813,7 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
     __shared__ K4Lds L;
 #ifdef KMC_CANON_PROF
     unsigned long long pacc[8] = {};
+    ProbeProf pp;
     PROF_T(tk0);
 #endif
     const int tid = threadIdx.x, lane = tid & 63;
@@ -840,11 +866,11 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
             uint32_t ncl = 0;
             PROF_T(ta);
             if (resident) {
-                wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl);
+                wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl PROF_PASS);
             } else {
                 for (uint64_t i0 = b0; i0 < e0; i0 += (uint64_t)kResKeys) {
                     load_keys(p.ent, i0, e0, kr);
-                    wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl);
+                    wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl PROF_PASS);
                 }
             }
             if (lane == 0) L.ncl[par][wv] = ncl;
@@ -927,7 +953,13 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
     }
 #ifdef KMC_CANON_PROF
     if (lane == 0)
+    {
         for (int i = 0; i < 8; ++i) atomicAdd(&g_prof[i], pacc[i]);
+        atomicAdd(&g_prof2[0], pp.rounds);
+        atomicAdd(&g_prof2[1], pp.keys);
+        atomicAdd(&g_prof2[2], pp.loops);
+        atomicAdd(&g_prof2[3], pp.cas);
+    }
 #endif
 }
 

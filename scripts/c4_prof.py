@@ -29,7 +29,7 @@ def main():
         print("iter %d: passes/wave %d lists/wave %d | per wave %.1f Mcycles: %s" % (
             it, v[6] // waves, v[7] // waves, tot / waves / 1e6,
             ", ".join("%s %.1f%%" % (n, 100.0 * v[i] / max(tot, 1)) for i, n in enumerate(names))))
-        print("   probe loops %d, rounds/loop %.2f, staged keys/loop %.1f" % (v[10], v[8] / max(v[10], 1), v[9] / max(v[10], 1)))
+        print("   probe loops %d, rounds/loop %.2f, staged keys/loop %.1f, CAS wait %.0f cycles/round (%.1f%% of wave time)" % (v[10], v[8] / max(v[10], 1), v[9] / max(v[10], 1), v[11] / max(v[8], 1), 100.0 * v[11] / max(tot, 1)))
 
 
 if __name__ == "__main__":
