@@ -674,10 +674,10 @@ struct K4Lds {
 };
 
 #ifdef KMC_CANON_PROF
-__device__ unsigned long long g_prof2[4];  // probe rounds, staged keys, probe loops, CAS-wait cycles
+__device__ unsigned long long g_prof2[8];  // probe rounds, staged keys, probe loops, CAS-wait, staging, probe, queue-read cycles
 // per-wave counters in registers, added to g_prof2 once per wave at the end
 struct ProbeProf {
-    unsigned long long rounds = 0, keys = 0, loops = 0, cas = 0;
+    unsigned long long rounds = 0, keys = 0, loops = 0, cas = 0, stage = 0, probe = 0, qread = 0;
 };
 #define PROF_PARAM , ProbeProf &pp
 #define PROF_PASS , pp
@@ -728,7 +728,14 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
         const uint32_t at = cursor + (uint32_t)__popcll(mn & lt);
         cursor += (uint32_t)__popcll(mn);
         const bool take = !busy && at < nq;
+#ifdef KMC_CANON_PROF
+        const unsigned long long tq = __builtin_amdgcn_s_memtime();
+        const unsigned long long nk = __hip_atomic_load(&qk[take ? at : 0u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp.qread += __builtin_amdgcn_s_memtime() - tq;
+#else
         const unsigned long long nk = qk[take ? at : 0u];
+#endif
         h = take ? nk : h;
         s = take ? ((uint32_t)nk & (kTableSlots - 1)) : s;
         step = take ? (((uint32_t)(nk >> kTableLg) & (kTableSlots - 1)) | 1u) : step;  // odd: visits every slot
@@ -783,6 +790,9 @@ __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes]
     unsigned long long *qk = L.qk[wv];
     int next = 0;  // first key slot not yet staged (wave-uniform)
     do {
+#ifdef KMC_CANON_PROF
+        const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+#endif
         uint32_t nq = 0;  // wave-uniform
 #pragma unroll
         for (int j = 0; j < kRes; ++j) {
@@ -795,7 +805,15 @@ __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes]
                 next = j + 1;
             }
         }
+#ifdef KMC_CANON_PROF
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+        pp.stage += ts1 - ts0;
+#endif
         if (nq) probe_staged(L, wv, nq, cap, ovf, ncl PROF_PASS);
+#ifdef KMC_CANON_PROF
+        pp.probe += __builtin_amdgcn_s_memtime() - ts1;
+#endif
     } while (next < kRes && ncl <= cap);
 }
 
@@ -959,6 +977,9 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         atomicAdd(&g_prof2[1], pp.keys);
         atomicAdd(&g_prof2[2], pp.loops);
         atomicAdd(&g_prof2[3], pp.cas);
+        atomicAdd(&g_prof2[4], pp.stage);
+        atomicAdd(&g_prof2[5], pp.probe);
+        atomicAdd(&g_prof2[6], pp.qread);
     }
 #endif
 }
@@ -1008,13 +1029,13 @@ extern "C" int kmc_diag_canon_claim_cap(unsigned cap) {
 }
 
 #ifdef KMC_CANON_PROF
-extern "C" int kmc_diag_canon_prof(unsigned long long *host12) {  // read and reset
-    if (hipMemcpyFromSymbol(host12, HIP_SYMBOL(g_prof), 64) != hipSuccess ||
-        hipMemcpyFromSymbol(host12 + 8, HIP_SYMBOL(g_prof2), 32) != hipSuccess)
+extern "C" int kmc_diag_canon_prof(unsigned long long *host16) {  // read and reset
+    if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_prof), 64) != hipSuccess ||
+        hipMemcpyFromSymbol(host16 + 8, HIP_SYMBOL(g_prof2), 64) != hipSuccess)
         return 1;
     unsigned long long z[8] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, 64) != hipSuccess ||
-           hipMemcpyToSymbol(HIP_SYMBOL(g_prof2), z, 32) != hipSuccess;
+           hipMemcpyToSymbol(HIP_SYMBOL(g_prof2), z, 64) != hipSuccess;
 }
 #endif
 
