@@ -125,12 +125,15 @@ def test_radix_k9_13_vs_oracle(kmc, oracle, cuda, k):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
-@pytest.mark.parametrize("k", [11, 12, 13])
+@pytest.mark.parametrize("k", [9, 10, 11, 12, 13])
 def test_radix_wrapping_bins_recounted(kmc, oracle, cuda, k):
     """k >= 12 keeps two 16-bit bins per LDS word in R4: a k-mer seen >= 65 536
     times in one list (poly-A / poly-AC runs) wraps its bin and the list is
-    recounted exactly; lists without a wrap keep the packed result (k = 11: the
-    32-bit bins, same input)."""
+    recounted exactly; lists without a wrap keep the packed result (k <= 11: the
+    32-bit bins, same input).  The same runs overflow R3's rings every round (one
+    bucket takes a whole round's windows): its cold path, the partly-written first
+    segment after an overflow and several segments per phase-B thread, at every
+    ring geometry (k = 9..13)."""
     rng = np.random.default_rng(4100 + k)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     poly = np.full(300_000, ord("A"), np.uint8)
