@@ -501,45 +501,78 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
 }
 
 // Records that span several workgroups: sum their slab slots; records without a
-// window in range get zeros.  Grid (ceil(W / 256), ny): blockIdx.x picks 256
-// slab words (W = 4^k, or 4^k / 2 packed words at k = 8, each holding bins c and
-// c | 0x8000), records s = blockIdx.y, blockIdx.y + ny, ... (the record count is
-// not bounded by the grid: gridDim.x * blockDim.x stays far below 2^32).
+// window in range get zeros.  Grid (NW / RW, ny): blockIdx.x picks RW = 4 * RC
+// slab words (NW = 4^k words, or 4^k / 2 packed words at k = 8, each holding bins
+// c and c | 0x8000), records s = blockIdx.y, blockIdx.y + ny, ...  The block first
+// lists the record's slots (slot_rec, in LDS), then RC columns of 16-byte loads x
+// RR rows of slots sum them with no dependent load in the loop, and the rows meet
+// in LDS.  (One thread per word walking the workgroups with a slot_rec test before
+// every slab load was latency-bound: 72 us for the ~205 slots of an 8-way shard's
+// record, against a 325 us histogram; scripts/shardbench.py.)
+constexpr int kRedList = 1024;  // slot candidates listed per chunk
 template <int K, class Idx, bool P16>
 __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     constexpr int NB = 1 << (2 * K);
     constexpr int NW = P16 ? NB / 2 : NB;
-    const int c = (int)blockIdx.x * 256 + threadIdx.x;
-    if (c >= NW) return;
+    constexpr int RC = NW / 4 < 16 ? NW / 4 : 16;  // 16-byte columns
+    constexpr int RR = 256 / RC;                   // rows over the slots
+    constexpr int RW = 4 * RC;                     // words per block
+    constexpr int NH = P16 ? 2 : 1;                // counters per word
+    __shared__ uint32_t s_list[kRedList];
+    __shared__ uint32_t s_n;
+    __shared__ uint32_t s_part[RR][RW * NH];
+    const int tid = threadIdx.x, col = tid % RC, row = tid / RC;
+    const int64_t c0 = (int64_t)blockIdx.x * RW;
     const Geom g = make_geom<Idx>(p);
     for (int64_t s = blockIdx.y; s < p.n; s += gridDim.y) {
         int64_t ca, ce;
         record_windows<K, Idx>(p, g, s, ca, ce);
         if (ce <= ca) {
-            p.sum[s + p.ld * (int64_t)c] = 0;
-            if (P16) p.sum[s + p.ld * (int64_t)(c + NW)] = 0;
+            for (int i = tid; i < RW * NH; i += 256) {
+                const int64_t c = c0 + i % RW + (i / RW) * NW;
+                p.sum[s + p.ld * c] = 0;
+            }
             continue;
         }
         const int64_t wf = ((ca >> kTileShift) - g.T0) / g.tpw;
         const int64_t wlast = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
         if (wf == wlast) continue;  // written directly by the count kernel
-        uint32_t lo = 0, hi = 0;
-        for (int64_t w = wf; w <= wlast; ++w) {
+        uint32_t acc[4 * NH] = {};
+        for (int64_t cb = 2 * wf; cb <= 2 * wlast + 1; cb += kRedList) {
+            const int64_t ce2 = (cb + kRedList) < (2 * wlast + 2) ? (cb + kRedList) : (2 * wlast + 2);
+            __syncthreads();  // the previous chunk's list is consumed
+            if (tid == 0) s_n = 0u;
+            __syncthreads();
+            for (int64_t j = cb + tid; j < ce2; j += 256)
+                if (p.slot_rec[j] == s) s_list[atomicAdd(&s_n, 1u)] = (uint32_t)(j - cb);
+            __syncthreads();
+            const uint32_t n = s_n;
+#pragma unroll 4
+            for (uint32_t i = row; i < n; i += RR) {
+                const uint4 v = reinterpret_cast<const uint4 *>(p.slab + (cb + s_list[i]) * NB + c0)[col];
+                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                if (p.slot_rec[2 * w + q] == s) {
-                    const uint32_t v = p.slab[(2 * w + q) * NB + c];
-                    if (P16) {
-                        lo += v & 0xFFFFu;
-                        hi += v >> 16;
+                for (int e = 0; e < 4; ++e) {
+                    if constexpr (P16) {
+                        acc[e] += x[e] & 0xFFFFu;  // bin c
+                        acc[4 + e] += x[e] >> 16;  // bin c + NW
                     } else {
-                        lo += v;
+                        acc[e] += x[e];
                     }
                 }
             }
         }
-        p.sum[s + p.ld * (int64_t)c] = (int32_t)lo;
-        if (P16) p.sum[s + p.ld * (int64_t)(c + NW)] = (int32_t)hi;
+#pragma unroll
+        for (int e = 0; e < 4 * NH; ++e) s_part[row][(e / 4) * RW + col * 4 + e % 4] = acc[e];
+        __syncthreads();
+        for (int i = tid; i < RW * NH; i += 256) {
+            uint32_t t = 0u;
+#pragma unroll 8
+            for (int r = 0; r < RR; ++r) t += s_part[r][i];
+            const int64_t c = c0 + i % RW + (i / RW) * NW;
+            p.sum[s + p.ld * c] = (int32_t)t;
+        }
+        __syncthreads();  // s_part is reused by the next record
     }
 }
 
@@ -826,7 +859,8 @@ int run_dense(const Request &q, hipStream_t st) {
         if (he != hipSuccess) return (int)he;
     }
     constexpr int NWR = Cfg<K>::P16 ? NB / 2 : NB;  // slab words per slot
-    const unsigned cb = (unsigned)((NWR + 255) / 256);
+    constexpr int RW = NWR / 4 < 16 ? NWR : 64;      // words per reduce block (its RW)
+    const unsigned cb = (unsigned)(NWR / RW);
     hipLaunchKernelGGL((reduce_dense_kernel<K, Idx, Cfg<K>::P16>), dim3(cb, (unsigned)std::min<int64_t>(q.n, kMaxGridY)),
                        dim3(256), 0, st, p);
     he = hipGetLastError();
