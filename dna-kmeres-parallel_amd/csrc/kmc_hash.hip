@@ -130,6 +130,9 @@ struct HParams {
     int64_t lists;
     uint32_t *err;           // set when a list exceeds what K4 can split
     uint32_t claim_cap;      // K4 claims per wave and pass (kClaimW; smaller only in tests)
+    uint32_t sort_cap;       // K4s takes lists of at most this many keys (kSortCap; 0 in tests: none)
+    uint64_t *defer;         // [lists][3] (list, begin, end) left to the table kernel by K4s
+    unsigned long long *ndefer;  // their number
     uint64_t *rec_off;       // [n + 1] output offsets
     uint64_t *out_keys;
     uint32_t *out_counts;
@@ -843,14 +846,17 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
     if (tid < 2) L.ovf[tid] = 0u;
     if (tid < 64) L.dummy[tid] = 0ull;
     lds_barrier();
-    const int64_t G = gridDim.x;
-    int64_t l = blockIdx.x;
-    if (l >= p.lists) return;
+    // the lists canon_sort_kernel left: longer than its capacity, or a key repeated
+    // more often than its dedup takes
+    const int64_t G = gridDim.x, nl = (int64_t)*p.ndefer;
+    const uint64_t *dl = p.defer;  // (list, begin, end) triples
+    int64_t i = blockIdx.x;
+    if (i >= nl) return;
     // list bounds two lists ahead, keys one list ahead
-    uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1], b1 = 0, e1 = 0;
-    if (l + G < p.lists) {
-        b1 = p.list_start[l + G];
-        e1 = p.list_start[l + G + 1];
+    uint64_t b0 = dl[3 * i + 1], e0 = dl[3 * i + 2], b1 = 0, e1 = 0;
+    if (i + G < nl) {
+        b1 = dl[3 * (i + G) + 1];
+        e1 = dl[3 * (i + G) + 2];
     }
     unsigned long long kr[kRes];
 #if KMC_CANON_KN
@@ -858,15 +864,16 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
     if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
 #endif
     int par = 0;
-    for (; l < p.lists; l += G) {
+    for (; i < nl; i += G) {
         PROF_T(t0);
+        const int64_t l = (int64_t)dl[3 * i];
         uint64_t b2 = 0, e2 = 0;
-        if (l + 2 * G < p.lists) {
-            b2 = p.list_start[l + 2 * G];
-            e2 = p.list_start[l + 2 * G + 1];
+        if (i + 2 * G < nl) {
+            b2 = dl[3 * (i + 2 * G) + 1];
+            e2 = dl[3 * (i + 2 * G) + 2];
         }
 #if KMC_CANON_KN
-        if (l + G < p.lists && e1 - b1 <= (uint64_t)kResKeys) load_keys(p.ent, b1, e1, kn);
+        if (i + G < nl && e1 - b1 <= (uint64_t)kResKeys) load_keys(p.ent, b1, e1, kn);
 #else
         if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
 #endif
@@ -984,6 +991,308 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
 #endif
 }
 
+// K4s (round 2): the common list, n <= sort_cap keys with no key repeated more than
+// kSortMaxM times, counted by a counting sort in LDS instead of the probed table:
+//   rank     one returning LDS add per key on its slot's 16-bit counter (slot =
+//            the low kSortSlotsLg bits of h, uniform: the list is cut by other bits)
+//   scan     exclusive prefix of the 8 192 counters (16 per thread, one block scan)
+//   scatter  key -> sk[start(slot) + rank]: the list sorted by slot
+//   dedup    position p (p = tid + 512 j: a wave reads consecutive keys) compares
+//            its key with the other keys of its slot (m - 1 of them, m ~ Poisson(<1));
+//            the first occurrence is emitted with the slot's count of its key,
+//            compacted per wave (one LDS add per wave and round)
+// Per key: 2 LDS atomics/reads + 1 scattered 8-byte write + ~m reads, 5 barriers per
+// list and no probe chains: the table kernel's CAS round trips (~21 cycles per wave
+// instruction) and pass structure are what bound it (section 4.4 of DESIGN.md).
+// A list that does not fit (longer than sort_cap, or a slot holding more than
+// kSortMaxM keys: a key repeated that often) is appended to p.defer and counted by
+// canon_table_kernel, which handles any length and any repeat count.
+constexpr int kSortBlock = 512;
+constexpr int kSortRes = 12;                          // keys per thread
+constexpr uint32_t kSortCap = 6080;                   // <= kSortBlock * kSortRes; LDS: 2 workgroups per CU
+constexpr int kSortSlotsLg = 13;
+constexpr int kSortSlots = 1 << kSortSlotsLg;         // 16-bit counters, two per word
+constexpr uint32_t kSortMaxM = 16;                    // keys per slot handled by the pairwise dedup
+constexpr uint32_t kHotMax = 128;                     // crowded slots per list handled by wave rounds
+static_assert(kSortCap <= (uint32_t)(kSortBlock * kSortRes) && kSortCap < 65536u, "K4s sizes");
+static_assert(kSortSlots / 2 == kSortBlock * 8, "K4s scan: 8 counter words per thread");
+
+struct K4sLds {
+    unsigned long long sk[kSortCap];  // the list, sorted by slot
+    uint32_t sc[kSortSlots / 2];      // slot counters, then slot starts (16-bit, packed)
+    uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
+    uint32_t wsum[kSortBlock / 64];
+    uint32_t out;                     // distinct keys emitted
+    uint32_t nhot;
+};
+
+// a list left to the table kernel: its id and key range
+__device__ __forceinline__ void defer_list(const HParams &p, int64_t l, uint64_t b, uint64_t e) {
+    const unsigned long long i = atomicAdd(p.ndefer, 1ull);
+    p.defer[3 * i] = (uint64_t)l;
+    p.defer[3 * i + 1] = b;
+    p.defer[3 * i + 2] = e;
+}
+
+// emits (h, cnt) at list offset o (the table kernel's pair format)
+__device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned long long h, uint32_t cnt) {
+    const uint32_t c = cnt - 1u;  // occurrences - 1, as the table kernel stores them
+    const unsigned long long tag = c < 3u ? c : 3u;
+    p.pk[o] = unmix64(h) | (tag << 62);
+    if (c >= 3u) p.pc[o] = cnt;
+}
+
+__device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t hi) { return hi ? (w >> 16) : (w & 0xFFFFu); }
+
+// diagnostic knobs (same-box A/B): KMC_SORT_PF 1 = the next list's keys loaded
+// during the dedup (kh live across lists), KMC_SORT_WRES 1 = one output reservation
+// per wave and list (first-occurrence bits and counts kept in registers)
+#ifndef KMC_SORT_PF
+#define KMC_SORT_PF 0
+#endif
+#ifndef KMC_SORT_WRES
+#define KMC_SORT_WRES 0
+#endif
+// timing-only ablations (results wrong): 1 = no dedup/emission, 2 = no scatter either,
+// 3 = no scan either (rank only), 4 = keys loaded, nothing else
+#ifndef KMC_SORT_ABL
+#define KMC_SORT_ABL 0
+#endif
+__global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_sort_kernel(HParams p) {
+    __shared__ __attribute__((aligned(16))) K4sLds S;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // keys of list l in registers; those of the next list are loaded once the
+    // current one is in LDS (after its scatter), so their latency hides behind the
+    // dedup
+    unsigned long long kh[kSortRes];
+    const auto load = [&](uint64_t b, uint32_t n) {
+#pragma unroll
+        for (int j = 0; j < kSortRes; ++j) {
+            const uint32_t i = (uint32_t)(j * kSortBlock + tid);
+            kh[j] = i < n ? p.ent[b + i] : kEmptyH;
+        }
+    };
+    const auto len = [&](uint64_t b, uint64_t e) { return (uint32_t)(e - b < 0xFFFFFFFFull ? e - b : 0xFFFFFFFFull); };
+    bool have = false;  // kh holds list l (workgroup-uniform)
+    for (int64_t l = blockIdx.x; l < p.lists; l += gridDim.x) {
+        const uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1];
+        const uint32_t n = len(b0, e0);
+        if (n > p.sort_cap) {  // workgroup-uniform
+            if (tid == 0) defer_list(p, l, b0, e0);
+            have = false;
+            continue;
+        }
+        if (!have) load(b0, n);
+        have = false;
+        if (KMC_SORT_ABL >= 4) {
+            if (tid == 0 && kh[0] == 1ull) p.ndist[l] = 0u;  // keeps the loads
+            continue;
+        }
+        reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
+        reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
+        lds_barrier();  // A: counters zero; the previous list's dedup is done
+        if (tid == 0) {
+            S.out = 0u;
+            S.nhot = 0u;
+        }
+        uint32_t rk[kSortRes / 2];  // ranks (< 2^16), two per register
+#pragma unroll
+        for (int j = 0; j < kSortRes; ++j) {
+            if ((j & 1) == 0) rk[j >> 1] = 0u;
+            if ((uint32_t)(j * kSortBlock + tid) < n) {
+                const uint32_t sl = (uint32_t)kh[j] & (kSortSlots - 1);
+                const uint32_t o = __hip_atomic_fetch_add(&S.sc[sl >> 1], (sl & 1u) ? 0x10000u : 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+                rk[j >> 1] |= half16(o, sl & 1u) << (16 * (j & 1));
+            }
+        }
+        lds_barrier();  // B: every key ranked
+        if (KMC_SORT_ABL >= 3) {
+            if (tid == 0 && S.sc[rk[0] & 4095u] == 7u) p.ndist[l] = 0u;
+            continue;
+        }
+        // scan: thread t owns counter words 8t .. 8t+7 (slots 16t .. 16t+15)
+        uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
+        uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
+        uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        uint32_t run = 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t c0 = w[i] & 0xFFFFu, c1 = w[i] >> 16;
+            if (__builtin_expect(c0 > kSortMaxM, 0)) {
+                const uint32_t x = atomicAdd(&S.nhot, 1u);
+                if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i;
+            }
+            if (__builtin_expect(c1 > kSortMaxM, 0)) {
+                const uint32_t x = atomicAdd(&S.nhot, 1u);
+                if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i + 1u;
+            }
+            w[i] = run | ((run + c0) << 16);  // exclusive starts, relative to the thread
+            run += c0 + c1;
+        }
+        uint32_t incl = run;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) S.wsum[wv] = incl;
+        lds_barrier();  // C1: wave totals
+        uint32_t base = incl - run;
+#pragma unroll
+        for (int v = 0; v < kSortBlock / 64; ++v) base += v < wv ? S.wsum[v] : 0u;
+        const uint32_t bb = base | (base << 16);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] += bb;  // starts < 2^16: no carry between the halves
+        reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
+        reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+        lds_barrier();  // C2: slot starts
+        const uint32_t nhot = S.nhot;
+        if (nhot > kHotMax) {  // too many crowded slots: the probed table counts this list (uniform)
+            if (tid == 0) defer_list(p, l, b0, e0);
+            continue;  // (the next list's barrier A orders the LDS reuse)
+        }
+#pragma unroll
+        for (int j = 0; j < kSortRes; ++j) {
+            if (KMC_SORT_ABL < 2 && (uint32_t)(j * kSortBlock + tid) < n) {
+                const uint32_t sl = (uint32_t)kh[j] & (kSortSlots - 1);
+                S.sk[half16(S.sc[sl >> 1], sl & 1u) + half16(rk[j >> 1], j & 1)] = kh[j];
+            }
+        }
+        if (KMC_SORT_PF && l + gridDim.x < p.lists) {  // the next list's keys, in flight during the dedup
+            const int64_t ln = l + gridDim.x;
+            const uint64_t bn = p.list_start[ln], en = p.list_start[ln + 1];
+            if (len(bn, en) <= p.sort_cap) {
+                load(bn, len(bn, en));
+                have = true;
+            }
+        }
+        lds_barrier();  // D: the list sorted by slot
+        if (KMC_SORT_ABL >= 1) {
+            if (tid == 0 && S.sk[0] == 1ull) p.ndist[l] = 0u;
+            continue;
+        }
+#if KMC_SORT_WRES
+        // dedup: first occurrences (bit j of fm) and their counts (4 bits each in
+        // cw: a normal slot holds at most kSortMaxM = 16 keys, stored as count - 1),
+        // then one output reservation per wave
+        uint32_t fm = 0u, wtot = 0u;
+        uint64_t cw = 0u;
+        static_assert(kSortRes * 4 <= 64, "K4s count bits");
+#pragma unroll 2
+        for (int j = 0; j < kSortRes; ++j) {
+            const uint32_t pos = (uint32_t)(j * kSortBlock + tid);
+            bool first = false;
+            uint32_t cnt = 1u;
+            unsigned long long h = 0;
+            // (a key of a crowded slot may already be marked by the wave counting it)
+            if (pos < n && (h = S.sk[pos]) != kEmptyH) {
+                const uint32_t sl = (uint32_t)h & (kSortSlots - 1);
+                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
+                const uint32_t e = sl + 1 < (uint32_t)kSortSlots ? half16(S.sc[(sl + 1) >> 1], (sl + 1) & 1u) : n;
+                if (e - a <= kSortMaxM) {  // crowded slots: the wave rounds below
+                    first = true;
+                    for (uint32_t q = a; q < e; ++q) {
+                        if (q == pos) continue;
+                        if (S.sk[q] == h) {
+                            ++cnt;
+                            first = first && q > pos;
+                        }
+                    }
+                }
+            }
+            fm |= first ? (1u << j) : 0u;
+            cw |= (uint64_t)(cnt - 1u) << (4 * j);
+            wtot += (uint32_t)__popcll(__ballot(first));
+        }
+        uint32_t wb = 0u;
+        if (lane == 0 && wtot) wb = atomicAdd(&S.out, wtot);
+        wb = (uint32_t)__shfl((int)wb, 0);
+        if (wtot) {
+#pragma unroll 1
+            for (int j = 0; j < kSortRes; ++j) {
+                const bool first = (fm >> j) & 1u;
+                const uint64_t m = __ballot(first);
+                if (first) {
+                    const uint32_t pos = (uint32_t)(j * kSortBlock + tid);
+                    emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), S.sk[pos], (uint32_t)((cw >> (4 * j)) & 15u) + 1u);
+                }
+                wb += (uint32_t)__popcll(m);
+            }
+        }
+#else
+        // dedup: the first occurrence of each key is emitted with its count, compacted
+        // per wave and round (one LDS add by lane 0)
+#pragma unroll 2
+        for (int j = 0; j < kSortRes; ++j) {
+            const uint32_t pos = (uint32_t)(j * kSortBlock + tid);
+            if (__builtin_amdgcn_readfirstlane(j * kSortBlock + wv * 64) >= (int)n) break;  // wave-uniform
+            bool first = false;
+            uint32_t cnt = 1u;
+            unsigned long long h = 0;
+            // (a key of a crowded slot may already be marked by the wave counting it)
+            if (pos < n && (h = S.sk[pos]) != kEmptyH) {
+                const uint32_t sl = (uint32_t)h & (kSortSlots - 1);
+                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
+                const uint32_t e = sl + 1 < (uint32_t)kSortSlots ? half16(S.sc[(sl + 1) >> 1], (sl + 1) & 1u) : n;
+                if (e - a <= kSortMaxM) {  // crowded slots: the wave rounds below
+                    first = true;
+                    for (uint32_t q = a; q < e; ++q) {
+                        if (q == pos) continue;
+                        if (S.sk[q] == h) {
+                            ++cnt;
+                            first = first && q > pos;
+                        }
+                    }
+                }
+            }
+            const uint64_t m = __ballot(first);
+            uint32_t wb = 0u;
+            if (lane == 0 && m) wb = atomicAdd(&S.out, (uint32_t)__popcll(m));
+            wb = (uint32_t)__shfl((int)wb, 0);
+            if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
+        }
+#endif
+        // crowded slots (a key repeated more than kSortMaxM times hashes there), one
+        // per wave: each round takes the first key not yet counted as the pivot, counts
+        // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
+        for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kSortBlock / 64) {
+            const uint32_t sl = S.hot[hs];
+            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
+            const uint32_t e = sl + 1 < (uint32_t)kSortSlots ? half16(S.sc[(sl + 1) >> 1], (sl + 1) & 1u) : n;
+            uint32_t c = a;
+            for (;;) {
+                unsigned long long piv = kEmptyH;
+                for (; c < e; c += 64) {
+                    const uint32_t q = c + (uint32_t)lane;
+                    const unsigned long long x = q < e ? S.sk[q] : kEmptyH;
+                    const uint64_t bal = __ballot(x != kEmptyH);
+                    if (bal) {
+                        const int f = __builtin_ctzll(bal);
+                        piv = (unsigned long long)__shfl((long long)x, f);
+                        c += (uint32_t)f;
+                        break;
+                    }
+                }
+                if (c >= e) break;  // wave-uniform
+                uint32_t cnt = 0u;
+                for (uint32_t q0 = c; q0 < e; q0 += 64) {
+                    const uint32_t q = q0 + (uint32_t)lane;
+                    const bool eq = q < e && S.sk[q] == piv;
+                    cnt += (uint32_t)__popcll(__ballot(eq));
+                    if (eq) S.sk[q] = kEmptyH;
+                }
+                if (lane == 0) emit_pair(p, b0 + atomicAdd(&S.out, 1u), piv, cnt);
+                ++c;
+            }
+        }
+        lds_barrier();  // E: every key emitted
+        if (tid == 0) p.ndist[l] = S.out;
+    }
+}
+
 // K5: pairs to their final place; record offsets
 __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
     const int64_t l = blockIdx.x;
@@ -1011,6 +1320,7 @@ struct HCache {
 std::mutex h_mu;
 std::vector<HCache> h_ws;
 uint32_t h_claim_cap = kClaimW;
+uint32_t h_sort_cap = kSortCap;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1025,6 +1335,14 @@ extern "C" int kmc_diag_canon_claim_cap(unsigned cap) {
     if (cap > (unsigned)kClaimW) return KMC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h_mu);
     h_claim_cap = cap ? cap : kClaimW;
+    return KMC_OK;
+}
+
+// Test hook (not in kmc.h): the longest list canon_sort_kernel takes (0: none, so
+// every list goes to canon_table_kernel); any value above kSortCap restores the default.
+extern "C" int kmc_diag_canon_sort_cap(unsigned cap) {
+    std::lock_guard<std::mutex> lk(h_mu);
+    h_sort_cap = cap > kSortCap ? kSortCap : cap;
     return KMC_OK;
 }
 
@@ -1129,6 +1447,8 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     const size_t o_nd = o; o += al256((size_t)L * 4);
     const size_t o_do = o; o += al256((size_t)(L + 1) * 8);
     const size_t o_err = o; o += al256(4);
+    const size_t o_dn = o; o += al256(8);
+    const size_t o_dl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
     const size_t total = o;
     char *ws;
     {
@@ -1165,6 +1485,9 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     p.dist_off = reinterpret_cast<uint64_t *>(ws + o_do);
     p.err = reinterpret_cast<uint32_t *>(ws + o_err);
     p.claim_cap = h_claim_cap;
+    p.sort_cap = h_sort_cap;
+    p.ndefer = reinterpret_cast<unsigned long long *>(ws + o_dn);
+    p.defer = reinterpret_cast<uint64_t *>(ws + o_dl);
     p.rec_off = rec_offsets;
     p.out_keys = keys;
     p.out_counts = counts;
@@ -1177,7 +1500,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
         (NF && (he = hipMemcpyAsync((void *)p.fsplit, fsplit.data(), NF * sizeof(int2), hipMemcpyHostToDevice,
                                     stream))))
         return (int)he;
-    if ((he = hipMemsetAsync(p.err, 0, 4, stream))) return (int)he;
+    if ((he = hipMemsetAsync(p.err, 0, 4, stream)) || (he = hipMemsetAsync(p.ndefer, 0, 8, stream))) return (int)he;
     if (M > 0) {
         if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream)) ||
             (he = hipMemsetAsync(p.cnt_c, 0, (size_t)Mc * 4, stream)))
@@ -1189,7 +1512,11 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     hipLaunchKernelGGL(canon_coarse_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
     hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (NF > 0) hipLaunchKernelGGL(canon_fine_kernel, dim3((unsigned)NF), dim3(kWalkBlock), 0, stream, p);
-    // persistent: two workgroups per CU (their tables fill the LDS) striding over the lists
+    // persistent, two workgroups per CU (64 KB of LDS each), striding over the lists
+    hipLaunchKernelGGL(canon_sort_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 2 * (int64_t)cus))),
+                       dim3(kSortBlock), 0, stream, p);
+    // the deferred lists (count on the device): two workgroups per CU (their tables
+    // fill the LDS) striding over them; workgroups beyond the count exit at once
     hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (1024 / kCountBlock) * (int64_t)cus))),
                        dim3(kCountBlock), 0, stream, p);
     excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);

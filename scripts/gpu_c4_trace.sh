@@ -7,7 +7,7 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 one() {  # name lib
   d=gpurun_out/c4t/$1
-  KMC_LIB=$2 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o t -- python3 scripts/cbench.py --configs ${CONFIGS:-c4} --iters 3 --cpu-sample-c4 0 --cpu-sample-c3 0 > $d.log 2>&1 || { tail -20 $d.log; exit 1; }
+  KMC_LIB=$2 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o t -- python3 scripts/cbench.py --configs ${CONFIGS:-c4} --iters 3 --cpu-sample-c4 0 --cpu-sample-c3 0 ${CB_ARGS:-} > $d.log 2>&1 || { tail -20 $d.log; exit 1; }
   grep '^{' $d.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$1 s_min %.4f s_med %.4f distinct %d' % (d['s_min'], d['s_med'], d.get('distinct', -1)))"
   python3 - $d <<'PY'
 import csv, glob, sys

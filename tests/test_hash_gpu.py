@@ -125,12 +125,41 @@ def test_canonical_pass_overflow_split(kmc, oracle, cuda, cap):
     idx = np.append(idx, data.size)
     hook = kmc.lib().kmc_diag_canon_claim_cap
     hook.argtypes = [ctypes.c_uint]
-    assert hook(cap) == 0
+    sort_cap = kmc.lib().kmc_diag_canon_sort_cap  # 0: every list to the table kernel
+    sort_cap.argtypes = [ctypes.c_uint]
+    assert hook(cap) == 0 and sort_cap(0) == 0
     try:
         for k in (21, 31):
             assert_same(gpu_canon(kmc, cuda, data, idx, k), oracle.count_canonical(data, idx, k), "cap=%d k=%d" % (cap, k))
     finally:
-        assert hook(0) == 0
+        assert hook(0) == 0 and sort_cap(1 << 30) == 0
+
+
+@pytest.mark.parametrize("scap", [0, 1, 2500, 1 << 30])
+def test_canonical_sort_and_table_paths(kmc, oracle, cuda, scap):
+    """Lists split between the counting-sort kernel (K4s: lists of at most scap keys,
+    no key more than 16 times in one of its slots) and the probed table kernel
+    (every other list): the same counts whatever the split.  Records with lists of
+    ~2-4 K keys, hot keys (a list deferred from K4s for a crowded slot), short
+    records (lists of a few keys)."""
+    import ctypes
+    rng = np.random.default_rng(5 + scap % 97)
+    data, idx = random_records(rng, [1_200_000, 9000, 40, 700_001], b"ACGTNacgt",
+                               (.2, .2, .2, .2, .04, .04, .04, .04, .04))
+    rep = np.frombuffer(b"ACGTTGCAAT" * 3000 + b"G" * 900 + b"ACGATCGATCGGA" * 400, dtype=np.uint8)
+    data = np.concatenate([data, rep, np.zeros(1, np.uint8)])
+    idx = np.append(idx, data.size)
+    sort_cap = kmc.lib().kmc_diag_canon_sort_cap
+    sort_cap.argtypes = [ctypes.c_uint]
+    assert sort_cap(scap) == 0
+    try:
+        for k in (17, 31):
+            for flags in (0, kmc.CANON_SOFTMASK):
+                got = gpu_canon(kmc, cuda, data, idx, k, flags)
+                exp = oracle.count_canonical(data, idx, k, soft=bool(flags & 1))
+                assert_same(got, exp, "scap=%d k=%d flags=%d" % (scap, k, flags))
+    finally:
+        assert sort_cap(1 << 30) == 0
 
 
 def test_canonical_size_independent_properties(kmc, cuda):
