@@ -1021,6 +1021,7 @@ struct K4sLds {
     unsigned long long sk[kSortCap];  // the list, sorted by slot
     uint32_t sc[kSortSlots / 2];      // slot counters, then slot starts (16-bit, packed)
     uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
+    uint16_t q[kSortBlock / 64][kSortRes * 64];  // per wave: positions of keys that share a slot
     uint32_t wsum[kSortBlock / 64];
     uint32_t out;                     // distinct keys emitted
     uint32_t nhot;
@@ -1044,59 +1045,48 @@ __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned
 
 __device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t hi) { return hi ? (w >> 16) : (w & 0xFFFFu); }
 
-// diagnostic knobs (same-box A/B): KMC_SORT_PF 1 = the next list's keys loaded
-// during the dedup (kh live across lists), KMC_SORT_WRES 1 = one output reservation
-// per wave and list (first-occurrence bits and counts kept in registers)
-#ifndef KMC_SORT_PF
-#define KMC_SORT_PF 0
-#endif
-#ifndef KMC_SORT_WRES
-#define KMC_SORT_WRES 0
-#endif
-// timing-only ablations (results wrong): 1 = no dedup/emission, 2 = no scatter either,
-// 3 = no scan either (rank only), 4 = keys loaded, nothing else
+// timing-only ablations (results wrong): 1 = no pairwise check / crowded slots,
+// 2 = no scatter either, 3 = no scan either (rank only), 4 = keys loaded, nothing else
 #ifndef KMC_SORT_ABL
 #define KMC_SORT_ABL 0
 #endif
+
+// start of slot sl's keys in sk (after the scan); slot kSortSlots ends at n
+__device__ __forceinline__ uint32_t slot_start(const K4sLds &S, uint32_t sl, uint32_t n) {
+    return sl < (uint32_t)kSortSlots ? half16(S.sc[sl >> 1], sl & 1u) : n;
+}
+
 __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_sort_kernel(HParams p) {
     __shared__ __attribute__((aligned(16))) K4sLds S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint64_t lt = (1ull << lane) - 1ull;
-    // keys of list l in registers; those of the next list are loaded once the
-    // current one is in LDS (after its scatter), so their latency hides behind the
-    // dedup
-    unsigned long long kh[kSortRes];
-    const auto load = [&](uint64_t b, uint32_t n) {
+    uint16_t *wq = S.q[wv];
+    for (int64_t l = blockIdx.x; l < p.lists; l += gridDim.x) {
+        const uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1];
+        const uint32_t n = (uint32_t)(e0 - b0 < 0xFFFFFFFFull ? e0 - b0 : 0xFFFFFFFFull);
+        if (n > p.sort_cap) {  // workgroup-uniform
+            if (tid == 0) defer_list(p, l, b0, e0);
+            continue;
+        }
+        unsigned long long kh[kSortRes];
 #pragma unroll
         for (int j = 0; j < kSortRes; ++j) {
             const uint32_t i = (uint32_t)(j * kSortBlock + tid);
-            kh[j] = i < n ? p.ent[b + i] : kEmptyH;
+            kh[j] = i < n ? p.ent[b0 + i] : kEmptyH;
         }
-    };
-    const auto len = [&](uint64_t b, uint64_t e) { return (uint32_t)(e - b < 0xFFFFFFFFull ? e - b : 0xFFFFFFFFull); };
-    bool have = false;  // kh holds list l (workgroup-uniform)
-    for (int64_t l = blockIdx.x; l < p.lists; l += gridDim.x) {
-        const uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1];
-        const uint32_t n = len(b0, e0);
-        if (n > p.sort_cap) {  // workgroup-uniform
-            if (tid == 0) defer_list(p, l, b0, e0);
-            have = false;
-            continue;
-        }
-        if (!have) load(b0, n);
-        have = false;
         if (KMC_SORT_ABL >= 4) {
             if (tid == 0 && kh[0] == 1ull) p.ndist[l] = 0u;  // keeps the loads
             continue;
         }
         reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
         reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
-        lds_barrier();  // A: counters zero; the previous list's dedup is done
+        lds_barrier();  // A: counters zero; the previous list is done
         if (tid == 0) {
             S.out = 0u;
             S.nhot = 0u;
         }
+        // rank: one returning add per key on its slot's 16-bit counter
         uint32_t rk[kSortRes / 2];  // ranks (< 2^16), two per register
 #pragma unroll
         for (int j = 0; j < kSortRes; ++j) {
@@ -1114,8 +1104,8 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
             continue;
         }
         // scan: thread t owns counter words 8t .. 8t+7 (slots 16t .. 16t+15)
-        uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
-        uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
+        const uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
+        const uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
         uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
         uint32_t run = 0u;
 #pragma unroll
@@ -1154,97 +1144,59 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
             if (tid == 0) defer_list(p, l, b0, e0);
             continue;  // (the next list's barrier A orders the LDS reuse)
         }
+        // scatter: a key alone in its slot (the common case: ~4 K keys over 8 192
+        // slots) is a distinct key of count 1 and leaves at once; the others go to
+        // sk, and those of slots with at most kSortMaxM keys to this wave's queue
+        // of keys to check against their slot
+        uint32_t qn = 0u;  // wave-uniform
 #pragma unroll
         for (int j = 0; j < kSortRes; ++j) {
+            bool alone = false, shared = false;
+            uint32_t pos = 0u;
             if (KMC_SORT_ABL < 2 && (uint32_t)(j * kSortBlock + tid) < n) {
                 const uint32_t sl = (uint32_t)kh[j] & (kSortSlots - 1);
-                S.sk[half16(S.sc[sl >> 1], sl & 1u) + half16(rk[j >> 1], j & 1)] = kh[j];
+                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
+                const uint32_t m = slot_start(S, sl + 1u, n) - a;
+                pos = a + half16(rk[j >> 1], j & 1);
+                alone = m == 1u;
+                if (!alone) {
+                    S.sk[pos] = kh[j];
+                    shared = m <= kSortMaxM;
+                }
             }
-        }
-        if (KMC_SORT_PF && l + gridDim.x < p.lists) {  // the next list's keys, in flight during the dedup
-            const int64_t ln = l + gridDim.x;
-            const uint64_t bn = p.list_start[ln], en = p.list_start[ln + 1];
-            if (len(bn, en) <= p.sort_cap) {
-                load(bn, len(bn, en));
-                have = true;
+            const uint64_t am = __ballot(alone);
+            if (am) {
+                uint32_t wb = 0u;
+                if (lane == 0) wb = atomicAdd(&S.out, (uint32_t)__popcll(am));
+                wb = (uint32_t)__shfl((int)wb, 0);
+                if (alone) emit_pair(p, b0 + wb + (uint32_t)__popcll(am & lt), kh[j], 1u);
             }
+            const uint64_t sm = __ballot(shared);
+            if (shared) wq[qn + (uint32_t)__popcll(sm & lt)] = (uint16_t)pos;
+            qn += (uint32_t)__popcll(sm);
         }
-        lds_barrier();  // D: the list sorted by slot
+        lds_barrier();  // D: the shared keys sorted by slot
         if (KMC_SORT_ABL >= 1) {
             if (tid == 0 && S.sk[0] == 1ull) p.ndist[l] = 0u;
             continue;
         }
-#if KMC_SORT_WRES
-        // dedup: first occurrences (bit j of fm) and their counts (4 bits each in
-        // cw: a normal slot holds at most kSortMaxM = 16 keys, stored as count - 1),
-        // then one output reservation per wave
-        uint32_t fm = 0u, wtot = 0u;
-        uint64_t cw = 0u;
-        static_assert(kSortRes * 4 <= 64, "K4s count bits");
-#pragma unroll 2
-        for (int j = 0; j < kSortRes; ++j) {
-            const uint32_t pos = (uint32_t)(j * kSortBlock + tid);
+        // the wave's queued keys, 64 at a time: the first occurrence in its slot is
+        // emitted with the slot's count of its key
+        for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
+            const bool act = q0 + (uint32_t)lane < qn;
             bool first = false;
             uint32_t cnt = 1u;
             unsigned long long h = 0;
-            // (a key of a crowded slot may already be marked by the wave counting it)
-            if (pos < n && (h = S.sk[pos]) != kEmptyH) {
+            if (act) {
+                const uint32_t pos = wq[q0 + lane];
+                h = S.sk[pos];
                 const uint32_t sl = (uint32_t)h & (kSortSlots - 1);
-                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
-                const uint32_t e = sl + 1 < (uint32_t)kSortSlots ? half16(S.sc[(sl + 1) >> 1], (sl + 1) & 1u) : n;
-                if (e - a <= kSortMaxM) {  // crowded slots: the wave rounds below
-                    first = true;
-                    for (uint32_t q = a; q < e; ++q) {
-                        if (q == pos) continue;
-                        if (S.sk[q] == h) {
-                            ++cnt;
-                            first = first && q > pos;
-                        }
-                    }
-                }
-            }
-            fm |= first ? (1u << j) : 0u;
-            cw |= (uint64_t)(cnt - 1u) << (4 * j);
-            wtot += (uint32_t)__popcll(__ballot(first));
-        }
-        uint32_t wb = 0u;
-        if (lane == 0 && wtot) wb = atomicAdd(&S.out, wtot);
-        wb = (uint32_t)__shfl((int)wb, 0);
-        if (wtot) {
-#pragma unroll 1
-            for (int j = 0; j < kSortRes; ++j) {
-                const bool first = (fm >> j) & 1u;
-                const uint64_t m = __ballot(first);
-                if (first) {
-                    const uint32_t pos = (uint32_t)(j * kSortBlock + tid);
-                    emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), S.sk[pos], (uint32_t)((cw >> (4 * j)) & 15u) + 1u);
-                }
-                wb += (uint32_t)__popcll(m);
-            }
-        }
-#else
-        // dedup: the first occurrence of each key is emitted with its count, compacted
-        // per wave and round (one LDS add by lane 0)
-#pragma unroll 2
-        for (int j = 0; j < kSortRes; ++j) {
-            const uint32_t pos = (uint32_t)(j * kSortBlock + tid);
-            if (__builtin_amdgcn_readfirstlane(j * kSortBlock + wv * 64) >= (int)n) break;  // wave-uniform
-            bool first = false;
-            uint32_t cnt = 1u;
-            unsigned long long h = 0;
-            // (a key of a crowded slot may already be marked by the wave counting it)
-            if (pos < n && (h = S.sk[pos]) != kEmptyH) {
-                const uint32_t sl = (uint32_t)h & (kSortSlots - 1);
-                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
-                const uint32_t e = sl + 1 < (uint32_t)kSortSlots ? half16(S.sc[(sl + 1) >> 1], (sl + 1) & 1u) : n;
-                if (e - a <= kSortMaxM) {  // crowded slots: the wave rounds below
-                    first = true;
-                    for (uint32_t q = a; q < e; ++q) {
-                        if (q == pos) continue;
-                        if (S.sk[q] == h) {
-                            ++cnt;
-                            first = first && q > pos;
-                        }
+                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
+                first = true;
+                for (uint32_t q = a; q < e; ++q) {  // 2 <= m <= kSortMaxM
+                    if (q != pos && S.sk[q] == h) {
+                        ++cnt;
+                        first = first && q > pos;
                     }
                 }
             }
@@ -1254,14 +1206,12 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
             wb = (uint32_t)__shfl((int)wb, 0);
             if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
         }
-#endif
         // crowded slots (a key repeated more than kSortMaxM times hashes there), one
         // per wave: each round takes the first key not yet counted as the pivot, counts
         // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
         for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kSortBlock / 64) {
             const uint32_t sl = S.hot[hs];
-            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
-            const uint32_t e = sl + 1 < (uint32_t)kSortSlots ? half16(S.sc[(sl + 1) >> 1], (sl + 1) & 1u) : n;
+            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
             uint32_t c = a;
             for (;;) {
                 unsigned long long piv = kEmptyH;

@@ -19,6 +19,6 @@ for r in csv.DictReader(open(f)):
 PY
 }
 one default "" || exit 1
-for f in dna-kmeres-parallel_amd/lib/variants/*.so; do [ -e "$f" ] || continue
+for f in dna-kmeres-parallel_amd/lib/variants/*.so; do [ -e "$f" ] && [ -z "$VAR_SKIP" ] || continue
   one $(basename $f .so) $PWD/$f || exit 1
 done
