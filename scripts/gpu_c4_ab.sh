@@ -7,6 +7,6 @@ grep passed gpurun_out/c4t/tests.log; grep "^default" gpurun_out/c4ab.log
 python3 scripts/c4_calls.py gpurun_out/c4t/default | sed -n '2p;$p'
 mkdir -p gpurun_out/c4v && rm -rf gpurun_out/c4v/*
 for f in dna-kmeres-parallel_amd/lib/variants/*.so; do [ -e "$f" ] || continue; v=$(basename $f .so)
-  KMC_LIB=$PWD/$f timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c4v/$v -o t -- python3 scripts/cbench.py --configs c4 --iters 2 --no-check --cpu-sample-c4 0 --cpu-sample-c3 0 > gpurun_out/c4v/$v.log 2>&1 || { tail -5 gpurun_out/c4v/$v.log; exit 1; }
-  echo "== $v"; python3 scripts/c4_calls.py gpurun_out/c4v/$v | tail -1
+  KMC_LIB=$PWD/$f timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c4v/$v -o t -- python3 scripts/cbench.py --configs ${VCFGS:-c4} --iters 2 --no-check --cpu-sample-c4 0 --cpu-sample-c3 0 > gpurun_out/c4v/$v.log 2>&1 || { tail -5 gpurun_out/c4v/$v.log; exit 1; }
+  echo "== $v"; python3 scripts/c4_calls.py gpurun_out/c4v/$v | sed -n "2p;\$p"
 done
