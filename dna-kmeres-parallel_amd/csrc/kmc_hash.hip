@@ -1243,15 +1243,31 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
     }
 }
 
-// K5: pairs to their final place; record offsets
+// K5: pairs to their final place; record offsets.  Four loads in flight per thread
+// (KMC_PLACE_U; 1 and 8 measured: C4R place 9.4 / 8.1 ms against 8.3, C4 within the
+// box noise; four consecutive pairs per thread with 16-byte stores: no gain either).
+#ifndef KMC_PLACE_U
+#define KMC_PLACE_U 4
+#endif
 __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
     const int64_t l = blockIdx.x;
     const uint64_t src = p.list_start[l], dst = p.dist_off[l], m = p.ndist[l];
-    for (uint64_t i = threadIdx.x; i < m; i += 256) {
-        const uint64_t x = p.pk[src + i];
-        const uint32_t tag = (uint32_t)(x >> 62);
-        p.out_keys[dst + i] = x & 0x3FFFFFFFFFFFFFFFull;
-        p.out_counts[dst + i] = tag < 3u ? tag + 1u : p.pc[src + i];
+    for (uint64_t i0 = threadIdx.x; i0 < m; i0 += 256 * KMC_PLACE_U) {
+        unsigned long long x[KMC_PLACE_U];
+#pragma unroll
+        for (int u = 0; u < KMC_PLACE_U; ++u) {
+            const uint64_t i = i0 + 256u * u;
+            x[u] = i < m ? p.pk[src + i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < KMC_PLACE_U; ++u) {
+            const uint64_t i = i0 + 256u * u;
+            if (i < m) {
+                const uint32_t tag = (uint32_t)(x[u] >> 62);
+                p.out_keys[dst + i] = x[u] & 0x3FFFFFFFFFFFFFFFull;
+                p.out_counts[dst + i] = tag < 3u ? tag + 1u : p.pc[src + i];
+            }
+        }
     }
 }
 
