@@ -40,7 +40,7 @@
 // k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
 // spill entries (0: no scans)
 #ifndef KMC_HM3_SCAN
-#define KMC_HM3_SCAN 64
+#define KMC_HM3_SCAN 256
 #endif
 
 namespace kmc {
