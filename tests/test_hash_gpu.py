@@ -162,6 +162,25 @@ def test_canonical_sort_and_table_paths(kmc, oracle, cuda, scap):
         assert sort_cap(1 << 30) == 0
 
 
+def test_canonical_crowded_list_deferred(kmc, oracle, cuda):
+    """K4s hands a list with more than 128 crowded slots (keys repeated > 16 times)
+    to the table kernel: records of one list each (< 4 K windows), made of a 200-bp
+    unit repeated 20 times (200 distinct keys x 20 copies), beside records whose
+    crowded slots stay within K4s (a 12-bp unit: a dozen keys, hundreds of copies)."""
+    rng = np.random.default_rng(31)
+    recs = []
+    for r in range(6):
+        unit = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=200 if r % 2 == 0 else 12)
+        reps = 20 if r % 2 == 0 else 300
+        recs.append(np.append(np.tile(unit, reps), np.uint8(0)))
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([x.size for x in recs])]).astype(np.int64)
+    for k in (21, 31):
+        exp = oracle.count_canonical(data, idx, k)
+        assert exp[1].max() >= 20
+        assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "k=%d" % k)
+
+
 def test_canonical_size_independent_properties(kmc, cuda):
     """64 Mbase: counts sum to the valid windows; canonical == forward folded by revcomp."""
     import torch
