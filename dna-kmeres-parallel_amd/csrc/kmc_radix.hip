@@ -31,9 +31,12 @@
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
-// tile prefetch depth of the scatter pass
+// tile prefetch depth of the count and scatter passes (plain loads: see kmc_stream.h)
 #ifndef KMC_RSCAT_PF
 #define KMC_RSCAT_PF 2
+#endif
+#ifndef KMC_RCOUNT_PF
+#define KMC_RCOUNT_PF 2
 #endif
 // tiles per wave in one R3 ring round (more: fewer barriers, more ring overflows)
 #ifndef KMC_RING_PROF
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         RCountOp<K> op{s_cnt + (lane & (kCountRep - 1))};
-        stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        stream_tiles<K, RCountOp<K>, KMC_RCOUNT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         __syncthreads();
         for (int b = tid; b < NBK; b += BLOCK) {
             const uint4 *r4 = reinterpret_cast<const uint4 *>(s_cnt + b * kCountRep);
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-        stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         op.finish();
         __syncthreads();
 #if KMC_RING_PROF

@@ -15,12 +15,15 @@
 #include <cstdint>
 
 // Tiles kept in flight per wave ahead of the one being counted, and whether the
-// once-read sequence stream uses non-temporal (nt) loads (diagnostic knobs).
+// once-read sequence stream uses non-temporal (nt) loads: defaults of the dense
+// histogram kernels (round 2, same-box A/B: PF 2 -> 3 and nt loads took k = 8 from
+// 2.32 to 2.24 ms and k = 1..7 down 2-4 %; profiles/r02_stream_pf_nt_ab.txt); the
+// radix walks pass their own (PF 2, plain loads: PF 3 + nt made C3 4 % slower).
 #ifndef KMC_PF
-#define KMC_PF 2
+#define KMC_PF 3
 #endif
 #ifndef KMC_NT
-#define KMC_NT 0
+#define KMC_NT 1
 #endif
 // Diagnostic builds only (scripts/kbench.py): KMC_ABLATE=1 replaces the
 // per-window work by a register XOR (codes still computed), KMC_ABLATE=2 also
@@ -226,11 +229,12 @@ __device__ __forceinline__ int64_t tile_base(int64_t t, int64_t rl) {
     return b > rl16 ? b : rl16;
 }
 
+template <int NT = KMC_NT>
 __device__ __forceinline__ uint4 load_tile_fast(__amdgpu_buffer_rsrc_t rsrc, int64_t base_off, int64_t t,
                                                 int lane) {
     const int64_t off = (t << kTileShift) - base_off + (int64_t)lane * 16;
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(uint32_t)off, 0, KMC_NT ? 2 : 0);
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(uint32_t)off, 0, NT ? 2 : 0);
     return make_uint4(x[0], x[1], x[2], x[3]);
 }
 
@@ -271,9 +275,10 @@ __device__ __forceinline__ uint4 mask_range(uint4 v, int64_t q, int64_t rl, int6
 // r[q+1]) or a load inside a branch make the compiler wait for the load it has
 // just issued (s_waitcnt vmcnt(0)) before the next decode, which leaves one tile
 // in flight per wave whatever KMC_PF says.
-template <int K, int PF_ = KMC_PF>
+template <int K, int PF_ = KMC_PF, int NT_ = KMC_NT>
 struct TileStream {
     static constexpr int PF = PF_;
+    static constexpr int NT = NT_;
     static constexpr int NS = PF + 1;
     const char *__restrict__ data;
     int64_t t0, ps, pe, rl, rh;
@@ -288,7 +293,7 @@ struct TileStream {
     __device__ __forceinline__ void step(int64_t i, int64_t per, Op &op) {
         const int64_t t = t0 + i;
         constexpr int SN = (S + 1) % NS, SL = (S + PF) % NS;
-        r[SL] = load_tile_fast(rsrc, base_off, t + PF, lane);
+        r[SL] = load_tile_fast<NT>(rsrc, base_off, t + PF, lane);
         if (tile_straddles(t + 1, rl, rh))
             r[SN] = mask_range(r[SN], ((t + 1) << kTileShift) + (int64_t)lane * 16, rl, rh);
         const uint4 r_cur = r[S], r_nxt = r[SN];
@@ -355,10 +360,10 @@ struct TileStream {
     }
 };
 
-template <int K, class Op, int PF = KMC_PF>
+template <int K, class Op, int PF = KMC_PF, int NT = KMC_NT>
 __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
                                              int64_t ps, int64_t pe, int64_t rl, int64_t rh, int lane, Op &op) {
-    using TS = TileStream<K, PF>;
+    using TS = TileStream<K, PF, NT>;
     const int64_t n = t1 > t0 ? t1 - t0 : 0;  // <= per
     if (n > 0) {
         TS ts;
@@ -374,7 +379,7 @@ __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int6
         ts.base_off = tile_base(t0, rl);
         ts.rsrc = tile_rsrc(data, ts.base_off, rh);
 #pragma unroll
-        for (int q = 0; q < TS::PF; ++q) ts.r[q] = load_tile_fast(ts.rsrc, ts.base_off, t0 + q, lane);
+        for (int q = 0; q < TS::PF; ++q) ts.r[q] = load_tile_fast<NT>(ts.rsrc, ts.base_off, t0 + q, lane);
         if (tile_straddles(t0, rl, rh)) ts.r[0] = mask_range(ts.r[0], (t0 << kTileShift) + (int64_t)lane * 16, rl, rh);
 #if KMC_ABLATE == 2
         ts.c_cur = ts.r[0].x ^ ts.r[0].y;
