@@ -1249,6 +1249,9 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
 #ifndef KMC_PLACE_U
 #define KMC_PLACE_U 4
 #endif
+#ifndef KMC_PLACE_NT
+#define KMC_PLACE_NT 0  // 1: non-temporal pair loads, 2: and output stores (same-box A/B: no gain)
+#endif
 __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
     const int64_t l = blockIdx.x;
     const uint64_t src = p.list_start[l], dst = p.dist_off[l], m = p.ndist[l];
@@ -1257,15 +1260,22 @@ __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
 #pragma unroll
         for (int u = 0; u < KMC_PLACE_U; ++u) {
             const uint64_t i = i0 + 256u * u;
-            x[u] = i < m ? p.pk[src + i] : 0ull;
+            x[u] = i < m ? (KMC_PLACE_NT ? __builtin_nontemporal_load(p.pk + src + i) : p.pk[src + i]) : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < KMC_PLACE_U; ++u) {
             const uint64_t i = i0 + 256u * u;
             if (i < m) {
                 const uint32_t tag = (uint32_t)(x[u] >> 62);
-                p.out_keys[dst + i] = x[u] & 0x3FFFFFFFFFFFFFFFull;
-                p.out_counts[dst + i] = tag < 3u ? tag + 1u : p.pc[src + i];
+                const uint64_t key = x[u] & 0x3FFFFFFFFFFFFFFFull;
+                const uint32_t cnt = tag < 3u ? tag + 1u : p.pc[src + i];
+                if (KMC_PLACE_NT >= 2) {
+                    __builtin_nontemporal_store(key, p.out_keys + dst + i);
+                    __builtin_nontemporal_store(cnt, p.out_counts + dst + i);
+                } else {
+                    p.out_keys[dst + i] = key;
+                    p.out_counts[dst + i] = cnt;
+                }
             }
         }
     }

@@ -38,6 +38,9 @@
 #ifndef KMC_RCOUNT_PF
 #define KMC_RCOUNT_PF 2
 #endif
+#ifndef KMC_R4_NT
+#define KMC_R4_NT 0  // 1: R4 reads the entries with non-temporal loads (same-box A/B: no gain)
+#endif
 // tiles per wave in one R3 ring round (more: fewer barriers, more ring overflows)
 #ifndef KMC_RING_PROF
 #define KMC_RING_PROF 0  // diagnostic: per-phase shader-clock cycles of workgroup 0 (printf)
@@ -500,8 +503,17 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
         // four 16-byte loads in flight per lane (64 KB per CU): one per iteration
         // left the loop waiting on HBM latency
         uint64_t i = threadIdx.x;
+#if KMC_R4_NT
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const auto ld = [&](uint64_t k) {
+            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(v + k));
+            return make_uint4(y[0], y[1], y[2], y[3]);
+        };
+#else
+        const auto ld = [&](uint64_t k) { return v[k]; };
+#endif
         for (; i + 3 * 1024 < nvec; i += 4 * 1024) {
-            const uint4 x0 = v[i], x1 = v[i + 1024], x2 = v[i + 2048], x3 = v[i + 3072];
+            const uint4 x0 = ld(i), x1 = ld(i + 1024), x2 = ld(i + 2048), x3 = ld(i + 3072);
             add8(x0);
             add8(x1);
             add8(x2);
