@@ -1012,7 +1012,10 @@ constexpr int kSortRes = 12;                          // keys per thread
 constexpr uint32_t kSortCap = 6080;                   // <= kSortBlock * kSortRes; LDS: 2 workgroups per CU
 constexpr int kSortSlotsLg = 13;
 constexpr int kSortSlots = 1 << kSortSlotsLg;         // 16-bit counters, two per word
-constexpr uint32_t kSortMaxM = 16;                    // keys per slot handled by the pairwise dedup
+#ifndef KMC_SORT_MAXM
+#define KMC_SORT_MAXM 16
+#endif
+constexpr uint32_t kSortMaxM = KMC_SORT_MAXM;         // keys per slot handled by the pairwise dedup
 constexpr uint32_t kHotMax = 128;                     // crowded slots per list handled by wave rounds
 static_assert(kSortCap <= (uint32_t)(kSortBlock * kSortRes) && kSortCap < 65536u, "K4s sizes");
 static_assert(kSortSlots / 2 == kSortBlock * 8, "K4s scan: 8 counter words per thread");
