@@ -1013,7 +1013,7 @@ constexpr uint32_t kSortCap = 6080;                   // <= kSortBlock * kSortRe
 constexpr int kSortSlotsLg = 13;
 constexpr int kSortSlots = 1 << kSortSlotsLg;         // 16-bit counters, two per word
 #ifndef KMC_SORT_MAXM
-#define KMC_SORT_MAXM 16
+#define KMC_SORT_MAXM 8
 #endif
 constexpr uint32_t kSortMaxM = KMC_SORT_MAXM;         // keys per slot handled by the pairwise dedup
 constexpr uint32_t kHotMax = 128;                     // crowded slots per list handled by wave rounds
