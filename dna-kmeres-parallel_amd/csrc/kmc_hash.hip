@@ -60,6 +60,10 @@
 #ifndef KMC_CANON_ABL
 #define KMC_CANON_ABL 0
 #endif
+// K3b: the next round's entries loaded before the current round is ranked (1)
+#ifndef KMC_FINE_PF
+#define KMC_FINE_PF 1
+#endif
 
 namespace kmc {
 namespace {
@@ -594,16 +598,31 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
     Ring8 rg;
     rg.init(&R, p.ent, lf, p.list_start[lb + (threadIdx.x >> (10 - lf))]);
     __syncthreads();
-    for (uint64_t i0 = a0; i0 < a1; i0 += 8 * kWalkBlock) {
-        unsigned long long v[8];
-        uint32_t bk[8], vm = 0u;
+    // the next round's entries are loaded before this round is ranked and flushed
+    // (KMC_FINE_PF; one workgroup per CU whose waves meet at every round's barriers
+    // would otherwise wait on HBM once per round)
+    unsigned long long xn[8];
+    const auto fetch = [&](uint64_t i0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
-            const unsigned long long x = i < a1 ? p.ent_c[i] : 0ull;
+            xn[j] = i < a1 ? p.ent_c[i] : 0ull;
+        }
+    };
+    if (KMC_FINE_PF) fetch(a0);
+    for (uint64_t i0 = a0; i0 < a1; i0 += 8 * kWalkBlock) {
+        unsigned long long v[8], x[8];
+        uint32_t bk[8], vm = 0u;
+        if (!KMC_FINE_PF) fetch(i0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = xn[j];
+        if (KMC_FINE_PF && i0 + 8 * kWalkBlock < a1) fetch(i0 + 8 * kWalkBlock);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
             vm |= i < a1 ? 1u << j : 0u;
-            bk[j] = (uint32_t)(x >> (64 - lg)) & (uint32_t)(F - 1);
-            v[j] = list_value(x);
+            bk[j] = (uint32_t)(x[j] >> (64 - lg)) & (uint32_t)(F - 1);
+            v[j] = list_value(x[j]);
         }
         rg.add<8>(v, bk, vm);
         rg.round_end();
