@@ -31,12 +31,17 @@
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
-// tile prefetch depth of the count and scatter passes (plain loads: see kmc_stream.h)
+// tile prefetch depth and nt loads of the count (R1) and scatter (R3) walks, each
+// from a same-box A/B: R1 PF 3 + nt 2.04-2.06 -> 1.95-2.01 ms; R3 PF 2-4 equal, and
+// nt loads made it slower
 #ifndef KMC_RSCAT_PF
 #define KMC_RSCAT_PF 2
 #endif
 #ifndef KMC_RCOUNT_PF
-#define KMC_RCOUNT_PF 2
+#define KMC_RCOUNT_PF 3
+#endif
+#ifndef KMC_RCOUNT_NT
+#define KMC_RCOUNT_NT 1
 #endif
 #ifndef KMC_R4_NT
 #define KMC_R4_NT 0  // 1: R4 reads the entries with non-temporal loads (same-box A/B: no gain)
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         RCountOp<K> op{s_cnt + (lane & (kCountRep - 1))};
-        stream_tiles<K, RCountOp<K>, KMC_RCOUNT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        stream_tiles<K, RCountOp<K>, KMC_RCOUNT_PF, KMC_RCOUNT_NT>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         __syncthreads();
         for (int b = tid; b < NBK; b += BLOCK) {
             const uint4 *r4 = reinterpret_cast<const uint4 *>(s_cnt + b * kCountRep);
