@@ -60,6 +60,10 @@
 #ifndef KMC_CANON_ABL
 #define KMC_CANON_ABL 0
 #endif
+// K1 / K3a: the next chunk's 48 bytes loaded before the current chunk is hashed (1)
+#ifndef KMC_WALK_PF
+#define KMC_WALK_PF 1
+#endif
 // K3b: the next round's entries loaded before the current round is ranked (1)
 #ifndef KMC_FINE_PF
 #define KMC_FINE_PF 1
@@ -215,17 +219,29 @@ __device__ __forceinline__ void chunk_codes(uint4 r, bool soft, uint32_t &code, 
 // The hashed keys of the (up to 16) valid windows starting in 16-byte chunk q of
 // record piece [ps, pe) (window starts) of a record whose terminator is at
 // rend - 1: bit j of the result is set when h[j] holds window q + j.
-__device__ __forceinline__ uint32_t chunk_keys(const HParams &p, int64_t q, int64_t ps, int64_t pe, int64_t rend,
-                                               unsigned long long (&h)[16]) {
+// The 48 bytes chunk_keys decodes for chunk q (its 16 window starts + 32 halo bytes),
+// loaded ahead of use by the input walks (KMC_WALK_PF)
+struct ChunkRaw {
+    uint4 r[3];
+};
+__device__ __forceinline__ ChunkRaw chunk_raw(const HParams &p, int64_t q) {
+    const int64_t hi_byte = p.idx[p.n];
+    ChunkRaw c;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c.r[i] = load16(p.data, q + 16 * i, hi_byte);
+    return c;
+}
+
+__device__ __forceinline__ uint32_t chunk_keys(const HParams &p, const ChunkRaw &raw, int64_t q, int64_t ps,
+                                               int64_t pe, int64_t rend, unsigned long long (&h)[16]) {
     const int k = p.k;
     const bool soft = p.flags & KMC_CANON_SOFTMASK;
     const bool fwd_only = p.flags & KMC_CANON_FORWARD;
     const uint64_t kmask = (1ull << (2 * k)) - 1;
     const uint64_t wmask = (1ull << k) - 1;
-    const int64_t hi_byte = p.idx[p.n];
     uint32_t cd[3], bd[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) chunk_codes(load16(p.data, q + 16 * i, hi_byte), soft, cd[i], bd[i]);
+    for (int i = 0; i < 3; ++i) chunk_codes(raw.r[i], soft, cd[i], bd[i]);
     const uint64_t lo64 = (uint64_t)cd[0] | ((uint64_t)cd[1] << 32);
     const uint64_t badm = (uint64_t)bd[0] | ((uint64_t)bd[1] << 16) | ((uint64_t)bd[2] << 32);
     const int64_t last = std::min<int64_t>(pe, rend - k);  // window starts < last
@@ -289,9 +305,15 @@ __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
         const int nb = 1 << lg;
         for (int b = threadIdx.x; b < nb; b += kWalkBlock) c[b] = 0u;
         __syncthreads();
-        for (int64_t q = ((ps >> 4) + threadIdx.x) << 4; q < pe; q += (int64_t)kWalkBlock << 4) {
+        const int64_t qs = (int64_t)kWalkBlock << 4;
+        int64_t q = ((ps >> 4) + threadIdx.x) << 4;
+        ChunkRaw nx;
+        if (KMC_WALK_PF && q < pe) nx = chunk_raw(p, q);
+        for (; q < pe; q += qs) {
             unsigned long long h[16];
-            const uint32_t vm = chunk_keys(p, q, ps, pe, rend, h);
+            const ChunkRaw cr = KMC_WALK_PF ? nx : chunk_raw(p, q);
+            if (KMC_WALK_PF && q + qs < pe) nx = chunk_raw(p, q + qs);  // the next chunk, in flight
+            const uint32_t vm = chunk_keys(p, cr, q, ps, pe, rend, h);
 #pragma unroll
             for (int j = 0; j < 16; ++j)
                 if ((vm >> j) & 1u)
@@ -550,11 +572,16 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
         uint64_t *dst = lg > lgc ? p.ent_c : p.ent;
         const auto bk = [lgc](unsigned long long x) { return lgc ? (uint32_t)(x >> (64 - lgc)) : 0u; };
         const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
+        ChunkRaw nx;
+        if (KMC_WALK_PF && c0 + threadIdx.x < c1) nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
         for (int64_t cb = c0; cb < c1; cb += kWalkBlock) {
             const int64_t c = cb + threadIdx.x;
             unsigned long long h[16];
             uint32_t vm = 0u;
-            if (c < c1) vm = chunk_keys(p, c << 4, ps, pe, rend, h);
+            ChunkRaw cr = nx;
+            if (!KMC_WALK_PF && c < c1) cr = chunk_raw(p, c << 4);
+            if (KMC_WALK_PF && c + kWalkBlock < c1) nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
+            if (c < c1) vm = chunk_keys(p, cr, c << 4, ps, pe, rend, h);
             if (lg > lgc)
                 staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return x; }, dst);
             else  // buckets are the lists
