@@ -43,6 +43,9 @@
 #ifndef KMC_RCOUNT_NT
 #define KMC_RCOUNT_NT 1
 #endif
+#ifndef KMC_R4_U
+#define KMC_R4_U 4  // R4 16-byte entry loads in flight per lane
+#endif
 #ifndef KMC_R4_NT
 #define KMC_R4_NT 0  // 1: R4 reads the entries with non-temporal loads (same-box A/B: no gain)
 #endif
@@ -517,12 +520,12 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
 #else
         const auto ld = [&](uint64_t k) { return v[k]; };
 #endif
-        for (; i + 3 * 1024 < nvec; i += 4 * 1024) {
-            const uint4 x0 = ld(i), x1 = ld(i + 1024), x2 = ld(i + 2048), x3 = ld(i + 3072);
-            add8(x0);
-            add8(x1);
-            add8(x2);
-            add8(x3);
+        for (; i + (KMC_R4_U - 1) * 1024 < nvec; i += KMC_R4_U * 1024) {
+            uint4 x[KMC_R4_U];
+#pragma unroll
+            for (int u = 0; u < KMC_R4_U; ++u) x[u] = ld(i + 1024u * u);
+#pragma unroll
+            for (int u = 0; u < KMC_R4_U; ++u) add8(x[u]);
         }
         for (; i < nvec; i += 1024) add8(v[i]);
         const uint64_t t = a + nvec * 8;
