@@ -60,8 +60,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="bases per CPU worker for the reference CPU baseline (0 = sized to ~15 s; -1 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_dense_k8_10gbase.json"),
-                    help="HBM traffic per launch measured by rocprofv3 --pmc (see profiles/)")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_dense_k8_shards.json"),
+                    help="HBM traffic per launch measured by rocprofv3 --pmc, per shard size (see profiles/)")
+    ap.add_argument("--allreduce-reps", type=int, default=20,
+                    help="N > 1: all-reduces timed alone after the timed region")
     return ap.parse_args(argv)
 
 
@@ -226,25 +228,28 @@ def cpu_model():
     return m
 
 
-def run_cpu_baseline(args, data, L, k, n_rec):
+def run_cpu_baseline(args, data, k):
+    """The reference CPU path on this rank's bytes of the job (the whole buffer at
+    N = 1, rank 0's shard otherwise): one worker per usable core, each on its own
+    S-base slice (slices spread over the held bytes; they overlap only when the
+    shard is smaller than threads x S)."""
     import numpy as np
     threads, node_cpus = usable_cores()
     if args.cpu_threads:
         threads = args.cpu_threads
+    held = int(data.numel())
     # one thread first: its rate sizes the per-worker sample to ~15 s of work
-    probe = np.append(data[: 4_000_000].cpu().numpy(), np.uint8(0))
+    probe = np.append(data[: min(4_000_000, held)].cpu().numpy(), np.uint8(0))
     rate1, kind, dt1, _ = cpu_baseline([probe], k, 1)
     S = args.cpu_sample or int(min(max(rate1 * 15.0, 1e6), 256e6))
-    host = []
-    for t in range(threads):
-        r = t % n_rec
-        off = r * (L + 1) + ((t // n_rec) * S) % max(L - S, 1)
-        host.append(np.append(data[off: off + S].cpu().numpy(), np.uint8(0)))  # one record of S bases
+    S = max(min(S, held), k)
+    step = (held - S) // max(threads - 1, 1) if threads > 1 else 0
+    host = [np.append(data[t * step: t * step + S].cpu().numpy(), np.uint8(0)) for t in range(threads)]
     rate, kind, dt, kmers = cpu_baseline(host, k, threads)
     return {
         "value": rate, "unit": "k-mers/s", "cores": threads, "kind": kind,
         "value_1thread": rate1, "node_cpus": node_cpus,
-        "sample": "%d workers x %d bases of the same synthetic records (%.1f s wall, %d k-mers), k=%d, the "
+        "sample": "%d workers x %d bases of this rank's synthetic records (%.1f s wall, %d k-mers), k=%d, the "
                   "reference's permutationsCountAll (substr + std::map, main.cu:636-646) built -O2 from "
                   "/root/reference; cores = the CPUs this process may use (affinity and cgroup quota; the "
                   "machine shows %d); value_1thread: 1 worker x %d bases (%.1f s); CPU: %s"
@@ -362,20 +367,92 @@ def main():
     # the int32 matrix it writes
     alg_bytes = (win_hi - win_lo) + 4 * nb * n_tot
     kern_ms = sum(b.elapsed_time(e) for b, e in ev) / args.steps
-    stats = torch.tensor([t1 - t0, kern_ms, -alg_bytes / (kern_ms * 1e-3) / 1e9], dtype=torch.float64, device=dev)
+    result = finalize(args, world, rank, backend, data, bufs[0], L, k, n_tot, (win_lo, win_hi), t1 - t0, kern_ms,
+                      alg_bytes, timer="cuda")
+    if rank == 0:
+        print(json.dumps(result), flush=True)
     if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms, achieved = float(stats[0]), float(stats[1]), -float(stats[2])  # max, max, min over ranks
+        dist.destroy_process_group()
+
+
+def measure_allreduce(like, reps, timer):
+    """Average time of one all-reduce (SUM) of a matrix shaped like the count
+    matrix, alone: not overlapped with counting, on a scratch tensor of zeros (so
+    repeated sums cannot overflow).  timer "cuda": HIP events on the current stream
+    around each synchronous dist.all_reduce (the collective's own stream joins the
+    current one before and after it); "host": wall time (the gloo CPU tests)."""
+    import torch
+    import torch.distributed as dist
+    x = torch.zeros_like(like)
+    dist.all_reduce(x)  # first call: communicator/channel setup, not timed
+    if timer == "cuda":
+        torch.cuda.synchronize()
+        st = torch.cuda.current_stream()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        dist.barrier()
+        for b, e in ev:
+            b.record(st)
+            dist.all_reduce(x)
+            e.record(st)
+        torch.cuda.synchronize()
+        return sum(b.elapsed_time(e) for b, e in ev) / reps
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_reduce(x)
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def over_ranks(world, vals, device):
+    """(max, ...) of per-rank floats over the job: every entry is maxed; pass -x
+    for a minimum."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
+def pmc_traffic(path, k, data_bytes):
+    """HBM bytes per launch of the histogram kernel over a shard of data_bytes
+    window bytes, measured by rocprofv3 PMC (profiles/pmc_*.json: one object or a
+    list of them, one per shard size); None when no measurement matches."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    for e in (pmc if isinstance(pmc, list) else [pmc]):
+        if e.get("k") == k and e.get("data_bytes") == data_bytes:
+            return e.get("hbm_bytes_per_launch")
+    return None
+
+
+def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed, kern_ms, alg_bytes, timer):
+    """Everything after the timed region, at every N: the all-reduce timed alone,
+    the max-over-ranks statistics, the reference CPU path on rank 0, and the JSON
+    line (returned on rank 0, None elsewhere).  tests/test_multi.py runs it with
+    gloo at world 2 on CPU tensors (timer "host")."""
+    import torch.distributed as dist
+    win_lo, win_hi = win
+    nb = 1 << (2 * k)
+    dev = matrix.device
+    ar_ms = measure_allreduce(matrix, args.allreduce_reps, timer) if world > 1 else 0.0
+    traffic = pmc_traffic(args.pmc, k, win_hi - win_lo)
+    achieved_rank = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # max over ranks of time-likes; min of achieved and of "traffic known" (as -x)
+    elapsed, kern_ms, ar_ms, neg_ach, neg_known, traffic_max = over_ranks(
+        world, [elapsed, kern_ms, ar_ms, -achieved_rank, -(1.0 if traffic is not None else 0.0),
+                float(traffic or 0.0)], dev)
+    achieved = -neg_ach
+    traffic = traffic_max if -neg_known > 0.5 else None  # every rank's shard size was measured
 
     kmers_per_step = n_tot * (L - k + 1)
     value = kmers_per_step * args.steps / elapsed
-    traffic = None
-    if world == 1 and os.path.exists(args.pmc):
-        with open(args.pmc) as f:
-            pmc = json.load(f)
-        if pmc.get("k") == k and pmc.get("data_bytes") == win_hi - win_lo:
-            traffic = pmc.get("hbm_bytes_per_launch")
-
+    # the whole job's algorithmic bytes per k-mer (SURVEY.md §8(d)): every input
+    # byte once + the int32 output once, over the windows
+    job_bytes = n_tot * (L + 1) + 4 * nb * n_tot
+    node_gbps = value * job_bytes / kmers_per_step / 1e9
     if args.scaling == "strong":
         par = ("one %.1f Gbase buffer cut into %d byte-range shard(s) (kmc_plan_shards, 4 KiB cuts, k-1 halo), "
                "RCCL all-reduce of the int32 count matrix overlapping the next step" % (n_tot * L / 1e9, world))
@@ -400,6 +477,8 @@ def main():
                         % (k, n_tot, L, n_tot * L / 1e9,
                            "split over the GPUs" if args.scaling == "strong" else "%d records per GPU" % args.records),
             "k": k, "total_records": n_tot, "record_len": L, "bins": nb, "parallelism": par,
+            "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else "none (1 GPU)",
         },
         "roofline": {
             "bound": "hbm",
@@ -411,16 +490,30 @@ def main():
             "kernel": "count_dense_kernel<%d> (HIP events around the histogram launch; slowest rank)" % k,
             "kernel_ms": kern_ms,
             "alg_bytes_per_launch": alg_bytes,
+            # the whole node: value x algorithmic bytes per k-mer of the job over N x peak
+            "node_achieved": node_gbps,
+            "node_peak": HBM_PEAK_GBPS * world,
+            "node_frac": node_gbps / (HBM_PEAK_GBPS * world),
+            "alg_bytes_per_kmer": job_bytes / kmers_per_step,
+        },
+        "allreduce": {
+            "ms": ar_ms,
+            "bytes": 4 * nb * n_tot,
+            "how": ("%d synchronous all-reduces (SUM, int32) of a matrix shaped like the count matrix, timed alone "
+                    "after the timed region with HIP events on the current stream (slowest rank); in the timed "
+                    "steps each all-reduce overlaps the next step's counting" % args.allreduce_reps)
+                   if world > 1 else "none (1 GPU)",
         },
     }
-    if rank == 0 and world == 1 and args.cpu_sample >= 0:
-        result["cpu_baseline"] = run_cpu_baseline(args, data, L, k, n_tot)
+    if world > 1:
+        dist.barrier()  # every rank's GPU work is done before rank 0 takes the host cores
+    if rank == 0 and args.cpu_sample >= 0:
+        result["cpu_baseline"] = run_cpu_baseline(args, data, k)
     if backend != "nccl":
         result["rehearsal"] = "KMC_BENCH_BACKEND=%s, %d ranks sharing device(s): not a measurement" % (backend, world)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        dist.barrier()
+    return result if rank == 0 else None
 
 
 if __name__ == "__main__":

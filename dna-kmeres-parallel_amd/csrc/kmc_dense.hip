@@ -55,8 +55,9 @@ struct Spill {
 };
 
 struct Params {
-    const char *data;
+    const char *data;        // 16-byte aligned (the caller's pointer rounded down)
     const void *indices;
+    int64_t ibias;           // added to every indices[] value: the caller's misalignment
     int64_t n;
     int32_t *sum;
     int64_t ld;
@@ -717,9 +718,18 @@ inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
 // Upper bound of the spill entries one workgroup can emit for `tiles` tiles: a
 // scan entry (HM 2) stands for >= T >= 4096 increments of one 16-bit field; a wrap
 // entry (HM 1) for 65 536, or pairs with one.
+// Entries per window, whatever the scan interval: a scan entry (HM 3 / HM 2) moves
+// a multiple of its threshold T >= 32768 (HM 3) or >= 4096 (HM 2) out of one field,
+// all of it increments of that field since its last scan; a wrap of the HM 1 recount
+// costs 65 536 increments and emits at most 3 entries.  The recount keeps the first
+// pass's scan entries (zeroed) beside its own, so HM 3 + recount emits at most
+// windows * (1/32768 + 3/65536) = windows * 5/65536 <= windows / 4096 entries.
+constexpr uint32_t kSpillWindowsPerEntry = 4096;
+static_assert(5u * kSpillWindowsPerEntry <= 65536u, "HM 3 scan + HM 1 recount entries exceed the spill cap");
+static_assert(KMC_HM3_SCAN >= 0, "scan interval");
 inline uint32_t spill_cap_for(int64_t tiles_per_wg) {
     const int64_t windows = tiles_per_wg * kTile;
-    return (uint32_t)(windows / 4096 + 64);
+    return (uint32_t)(windows / kSpillWindowsPerEntry + 64);
 }
 
 struct Plan {
@@ -772,8 +782,9 @@ int cached_workspace(int device, size_t need, void **out) {
 }
 
 struct Request {
-    const char *data;
+    const char *data;        // 16-byte aligned
     const void *indices;
+    int64_t ibias;           // see Params
     int64_t n;
     int32_t *sum;
     int64_t ld;
@@ -799,8 +810,8 @@ int run_dense(const Request &q, hipStream_t st) {
             he = hipMemcpyAsync(&ends[1], (const Idx *)q.indices + q.n, sizeof(Idx), hipMemcpyDeviceToHost, st);
         if (he == hipSuccess) he = hipStreamSynchronize(st);
         if (he != hipSuccess) return (int)he;
-        wl = rl = (int64_t)ends[0];
-        wh = rh = (int64_t)ends[1];
+        wl = rl = (int64_t)ends[0] + q.ibias;
+        wh = rh = (int64_t)ends[1] + q.ibias;
         derive = false;
     }
     Plan pl;
@@ -817,6 +828,7 @@ int run_dense(const Request &q, hipStream_t st) {
     Params p;
     p.data = q.data;
     p.indices = q.indices;
+    p.ibias = q.ibias;
     p.n = q.n;
     p.sum = q.sum;
     p.ld = q.ld;
@@ -939,9 +951,13 @@ extern "C" int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, un
                                                     hipStream_t stream) {
     if (num_seqs == 0) return KMC_OK;
     if (!data || !indices || !sum) return KMC_ERR_INVALID_ARG;
-    if (reinterpret_cast<uintptr_t>(data) & 15u) return KMC_ERR_ALIGNMENT;
+    // kernels.h:113 takes any char *: a pointer inside a buffer (data + off) is
+    // rounded down to 16 bytes and the offsets biased by the difference (the
+    // aligned block holding data[0] lies in data's own page)
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(data) & 15u;
     Request q{};
-    q.data = data;
+    q.data = data - mis;
+    q.ibias = (int64_t)mis;
     q.indices = indices;
     q.n = num_seqs;
     q.sum = sum;
@@ -950,27 +966,47 @@ extern "C" int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, un
     return dispatch<int>(KMC_DROPIN_K, q, stream);
 }
 
-extern "C" size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *a, int device) {
-    if (!a || a->k < 1 || a->k > KMC_DENSE_MAX_K) return 0;
+// An unaligned data pointer (kernels.h:113 takes any char *): data rounded down to
+// 16 bytes, every range and record offset moved up by the difference.
+static kmc_dense_args aligned_args(const kmc_dense_args *a, int64_t &bias) {
+    kmc_dense_args b = *a;
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(a->data) & 15u;
+    b.data = a->data - mis;
+    b.read_lo += mis;
+    b.read_hi += mis;
+    b.win_lo += mis;
+    b.win_hi += mis;
+    bias = (int64_t)mis;
+    return b;
+}
+
+extern "C" size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *a0, int device) {
+    if (!a0 || a0->k < 1 || a0->k > KMC_DENSE_MAX_K) return 0;
+    int64_t bias = 0;
+    const kmc_dense_args al = aligned_args(a0, bias);
+    const kmc_dense_args *a = &al;
     if (a->k > 8) {
         size_t sz = 0;
-        return radix_dense(a, nullptr, true, &sz) == 0 ? sz : 0;
+        return radix_dense(a, bias, nullptr, true, &sz) == 0 ? sz : 0;
     }
     const int64_t wl = (int64_t)a->win_lo, wh = (int64_t)a->win_hi;
     return workspace_for<int64_t>(a->k, device, false, wl, wh);
 }
 
-extern "C" int kmc_count_dense_ex(const kmc_dense_args *a, hipStream_t stream) {
-    if (!a) return KMC_ERR_INVALID_ARG;
-    if (a->k < 1 || a->k > KMC_DENSE_MAX_K) return KMC_ERR_UNSUPPORTED_K;
-    if (a->num_seqs == 0) return KMC_OK;
-    if (!a->data || !a->indices || !a->sum) return KMC_ERR_INVALID_ARG;
-    if (reinterpret_cast<uintptr_t>(a->data) & 15u) return KMC_ERR_ALIGNMENT;
-    if (a->read_hi < a->read_lo || a->win_hi < a->win_lo) return KMC_ERR_INVALID_ARG;
-    if (a->sum_ld != 0 && a->sum_ld < a->num_seqs) return KMC_ERR_INVALID_ARG;
-    if (a->k > 8) return radix_dense(a, stream, false, nullptr);
+extern "C" int kmc_count_dense_ex(const kmc_dense_args *a0, hipStream_t stream) {
+    if (!a0) return KMC_ERR_INVALID_ARG;
+    if (a0->k < 1 || a0->k > KMC_DENSE_MAX_K) return KMC_ERR_UNSUPPORTED_K;
+    if (a0->num_seqs == 0) return KMC_OK;
+    if (!a0->data || !a0->indices || !a0->sum) return KMC_ERR_INVALID_ARG;
+    if (a0->read_hi < a0->read_lo || a0->win_hi < a0->win_lo) return KMC_ERR_INVALID_ARG;
+    if (a0->sum_ld != 0 && a0->sum_ld < a0->num_seqs) return KMC_ERR_INVALID_ARG;
+    int64_t bias = 0;
+    const kmc_dense_args al = aligned_args(a0, bias);
+    const kmc_dense_args *a = &al;
+    if (a->k > 8) return radix_dense(a, bias, stream, false, nullptr);
     Request q{};
     q.data = a->data;
+    q.ibias = bias;
     q.indices = a->indices;
     q.n = (int64_t)a->num_seqs;
     q.sum = a->sum;
@@ -988,15 +1024,18 @@ extern "C" int kmc_count_dense_ex(const kmc_dense_args *a, hipStream_t stream) {
 
 extern "C" size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device) {
     if (k < 1 || k > KMC_DENSE_MAX_K) return 0;
+    // the size for the most demanding alignment (a misaligned pointer moves the
+    // ranges up to 15 bytes, which can add a tile)
     if (k > 8) {
         kmc_dense_args a{};
         a.k = k;
         a.num_seqs = num_seqs;
-        a.read_hi = a.win_hi = data_bytes;
+        a.read_lo = a.win_lo = 15;
+        a.read_hi = a.win_hi = data_bytes + 15;
         size_t sz = 0;
-        return radix_dense(&a, nullptr, true, &sz) == 0 ? sz : 0;
+        return radix_dense(&a, 15, nullptr, true, &sz) == 0 ? sz : 0;
     }
-    return workspace_for<int64_t>(k, device, false, 0, (int64_t)data_bytes);
+    return workspace_for<int64_t>(k, device, false, 15, (int64_t)data_bytes + 15);
 }
 
 extern "C" int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,

@@ -55,11 +55,6 @@
 #ifndef KMC_CANON_RES
 #define KMC_CANON_RES 16
 #endif
-// Diagnostic builds only (scripts/gpu_c4_trace.sh): 1 = K4 inserts nothing, 2 = K4
-// writes no pairs.  Results are wrong.
-#ifndef KMC_CANON_ABL
-#define KMC_CANON_ABL 0
-#endif
 // K1 / K3a: the next chunk's 48 bytes loaded before the current chunk is hashed (1)
 #ifndef KMC_WALK_PF
 #define KMC_WALK_PF 1
@@ -89,9 +84,6 @@ constexpr int kCountBlock = KMC_CANON_BLOCK;  // K4 threads per workgroup (1024 
 constexpr int kTableLg = KMC_CANON_TLG;
 constexpr int kTableSlots = 1 << kTableLg;   // K4 LDS table: 4 096 x (8 + 4) B, double hashing
 constexpr int kWaves4 = kCountBlock / 64;
-#ifndef KMC_CANON_KN
-#define KMC_CANON_KN 0  // 1: K4 prefetches the next list's keys into registers (no gain: the CU's other workgroup hides the load)
-#endif
 #ifndef KMC_CANON_STAGE
 #define KMC_CANON_STAGE 320
 #endif
@@ -159,9 +151,6 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t h) {  // MurmurHash3 finalis
 // multiplicative hash (one 64-bit multiply, invertible) instead of fmix64 in
 // the two input walks; K3b (or K3a for single-list buckets) turns it into
 // fmix64(key) when writing the lists, which is what K4 hashes and unmixes.
-#ifndef KMC_CANON_MULPART
-#define KMC_CANON_MULPART 1
-#endif
 constexpr uint64_t kMulC = 0x9E3779B97F4A7C15ull, kMulCinv = 0xF1DE83E19937733Dull;
 __device__ __forceinline__ uint64_t part_of(uint64_t key);
 __device__ __forceinline__ uint64_t list_value(uint64_t m);
@@ -175,20 +164,10 @@ __device__ __forceinline__ uint64_t unmix64(uint64_t h) {  // inverse of fmix64
     return h;
 }
 
-__device__ __forceinline__ uint64_t part_of(uint64_t key) {
-#if KMC_CANON_MULPART
-    return key * kMulC;
-#else
-    return fmix64(key);
-#endif
-}
+__device__ __forceinline__ uint64_t part_of(uint64_t key) { return key * kMulC; }
 
 __device__ __forceinline__ uint64_t list_value(uint64_t m) {  // partition value -> fmix64(key)
-#if KMC_CANON_MULPART
     return fmix64(m * kMulCinv);
-#else
-    return m;
-#endif
 }
 
 // LE 2-bit code (first base in the low bits, the dense path's order) -> MSB-first
@@ -409,7 +388,7 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
     // thread reaches after this write-out
 }
 
-// Ring scatter of 8-byte entries (K3b, KMC_CANON_RING): the same scheme as
+// Ring scatter of 8-byte entries (K3b): the same scheme as
 // the radix path's R3 (kmc_radix.hip): a ring of RING = 16 384 / nbk entries per
 // bucket in LDS (128 KB in all), entries appended by one returning LDS add on the
 // bucket's word W[b] (ring half base << 16 | fill of the current 8-entry segment +
@@ -544,10 +523,6 @@ struct Ring8 {
     }
 };
 
-#ifndef KMC_CANON_RING
-#define KMC_CANON_RING 1
-#endif
-
 // (A ring version of K3a, as K3b's below, measured 10.5 -> 11.5 ms per C4 call: K3a
 // is bound by the key hashing of its input walk, and the rings' 8-entry rounds
 // need 4 barriers per 16 K windows against the staged sort's 3.)
@@ -610,7 +585,6 @@ __global__ void canon_list_start_kernel(HParams p) {
     p.list_start[l] = p.off[p.cbase[a] + (l - p.lbase[a]) * p.nwg[a]];
 }
 
-#if KMC_CANON_RING
 // K3b: one workgroup per coarse bucket of a record with several lists per bucket;
 // the bucket's entries (ent_c) to its lists (ent), 8 K entries per round through
 // the LDS rings (Ring8)
@@ -656,39 +630,6 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
     }
     rg.finish();
 }
-#else
-// K3b: one workgroup per coarse bucket of a record with several lists per bucket;
-// the bucket's entries (ent_c) to its lists (ent)
-__global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
-    __shared__ unsigned long long s_stage[kRound];
-    __shared__ uint32_t s_cnt[2][kMaxBk + 1];
-    __shared__ unsigned long long s_cur[kMaxBk], s_del[kMaxBk];
-    const Stage st{s_stage, s_cnt, s_cur, s_del};
-    const int2 rc = p.fsplit[blockIdx.x];
-    const int lg = p.lg[rc.x], lgc = coarse_lg(lg);
-    const int F = 1 << (lg - lgc);
-    const int64_t lb = p.lbase[rc.x] + (int64_t)rc.y * F;
-    const uint64_t a0 = p.list_start[lb], a1 = p.list_start[lb + F];
-    for (int f = threadIdx.x; f < F; f += kWalkBlock) s_cur[f] = p.list_start[lb + f];
-    for (int b = threadIdx.x; b < 2 * (kMaxBk + 1); b += kWalkBlock) (&s_cnt[0][0])[b] = 0u;
-    __syncthreads();
-    const auto bk = [lg, F](unsigned long long x) { return (uint32_t)(x >> (64 - lg)) & (uint32_t)(F - 1); };
-    int par = 0;
-    for (uint64_t i0 = a0; i0 < a1; i0 += kRound) {
-        unsigned long long h[16];
-        uint32_t vm = 0u;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
-            h[j] = i < a1 ? p.ent_c[i] : 0ull;
-            vm |= i < a1 ? 1u << j : 0u;
-        }
-        staged_round(st, par, F, h, vm, bk, [](unsigned long long x) { return list_value(x); }, p.ent);
-        par ^= 1;
-    }
-}
-
-#endif
 
 // K4: lists counted in an LDS table, workgroups striding over the lists.  Its
 // barriers are LDS-only (lds_barrier): __syncthreads would also wait for the pair
@@ -722,18 +663,6 @@ struct K4Lds {
     unsigned long long dummy[64];                // per lane: CAS target of an idle lane
 };
 
-#ifdef KMC_CANON_PROF
-__device__ unsigned long long g_prof2[8];  // probe rounds, staged keys, probe loops, CAS-wait, staging, probe, queue-read cycles
-// per-wave counters in registers, added to g_prof2 once per wave at the end
-struct ProbeProf {
-    unsigned long long rounds = 0, keys = 0, loops = 0, cas = 0, stage = 0, probe = 0, qread = 0;
-};
-#define PROF_PARAM , ProbeProf &pp
-#define PROF_PASS , pp
-#else
-#define PROF_PARAM
-#define PROF_PASS
-#endif
 // LDS byte offset of a __shared__ object
 template <class T>
 __device__ __forceinline__ uint32_t lds_off(T *p) {
@@ -758,10 +687,7 @@ __device__ __forceinline__ unsigned long long lds_cas64(uint32_t off, unsigned l
 // raises *ovf and stops (the pass is redone split in two), which also bounds the
 // table's load below one: no probe chain can wrap.
 __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint32_t cap, uint32_t *ovf,
-                                             uint32_t &ncl PROF_PARAM) {
-#ifdef KMC_CANON_PROF
-    uint32_t rounds = 0;
-#endif
+                                             uint32_t &ncl) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     const unsigned long long *qk = L.qk[wv];
@@ -777,29 +703,13 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
         const uint32_t at = cursor + (uint32_t)__popcll(mn & lt);
         cursor += (uint32_t)__popcll(mn);
         const bool take = !busy && at < nq;
-#ifdef KMC_CANON_PROF
-        const unsigned long long tq = __builtin_amdgcn_s_memtime();
-        const unsigned long long nk = __hip_atomic_load(&qk[take ? at : 0u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        pp.qread += __builtin_amdgcn_s_memtime() - tq;
-#else
         const unsigned long long nk = qk[take ? at : 0u];
-#endif
         h = take ? nk : h;
         s = take ? ((uint32_t)nk & (kTableSlots - 1)) : s;
         step = take ? (((uint32_t)(nk >> kTableLg) & (kTableSlots - 1)) | 1u) : step;  // odd: visits every slot
         busy = busy || take;
         if (!__ballot(busy)) break;
-#ifdef KMC_CANON_PROF
-        ++rounds;
-#endif
-#ifdef KMC_CANON_PROF
-        const unsigned long long tcas = __builtin_amdgcn_s_memtime();
-#endif
         const unsigned long long cur = lds_cas64(busy ? tk0 + 8u * s : dummy, kEmptyH, h);
-#ifdef KMC_CANON_PROF
-        pp.cas += __builtin_amdgcn_s_memtime() - tcas;
-#endif
         const bool claimed = busy && cur == kEmptyH;  // first occurrence (tc holds occurrences - 1)
         const bool dup = busy && cur == h;
         if (__ballot(dup)) {
@@ -816,11 +726,6 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
             break;
         }
     }
-#ifdef KMC_CANON_PROF
-    pp.rounds += rounds;
-    pp.keys += nq;
-    pp.loops += 1;
-#endif
 }
 
 // Pass of h among P: the P-quantile of h's bits [32, kPassTop) (above them: the
@@ -833,15 +738,12 @@ __device__ __forceinline__ uint32_t pass_of(unsigned long long h, uint32_t P) {
 // The wave's keys of pass q / P, staged in its LDS queue and probed; a queue that
 // fills up (repeats beyond the pass target) is probed and refilled.
 __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes], uint32_t q, uint32_t P, K4Lds &L,
-                                            int wv, uint32_t cap, uint32_t *ovf, uint32_t &ncl PROF_PARAM) {
+                                            int wv, uint32_t cap, uint32_t *ovf, uint32_t &ncl) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long *qk = L.qk[wv];
     int next = 0;  // first key slot not yet staged (wave-uniform)
     do {
-#ifdef KMC_CANON_PROF
-        const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-#endif
         uint32_t nq = 0;  // wave-uniform
 #pragma unroll
         for (int j = 0; j < kRes; ++j) {
@@ -854,35 +756,13 @@ __device__ __forceinline__ void wave_insert(const unsigned long long (&kh)[kRes]
                 next = j + 1;
             }
         }
-#ifdef KMC_CANON_PROF
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
-        pp.stage += ts1 - ts0;
-#endif
-        if (nq) probe_staged(L, wv, nq, cap, ovf, ncl PROF_PASS);
-#ifdef KMC_CANON_PROF
-        pp.probe += __builtin_amdgcn_s_memtime() - ts1;
-#endif
+        if (nq) probe_staged(L, wv, nq, cap, ovf, ncl);
     } while (next < kRes && ncl <= cap);
 }
 
-#ifdef KMC_CANON_PROF
-// diagnostic build only: per-phase s_memtime cycles of K4, summed over waves
-__device__ unsigned long long g_prof[8];
-#define PROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define PROF_ACC(i, d) pacc[i] += (d)
-#else
-#define PROF_T(v)
-#define PROF_ACC(i, d)
-#endif
 
 __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_table_kernel(HParams p) {
     __shared__ K4Lds L;
-#ifdef KMC_CANON_PROF
-    unsigned long long pacc[8] = {};
-    ProbeProf pp;
-    PROF_T(tk0);
-#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     for (int i = tid; i < kTableSlots; i += kCountBlock) {
@@ -905,24 +785,15 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         e1 = dl[3 * (i + G) + 2];
     }
     unsigned long long kr[kRes];
-#if KMC_CANON_KN
-    unsigned long long kn[kRes];
-    if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
-#endif
     int par = 0;
     for (; i < nl; i += G) {
-        PROF_T(t0);
         const int64_t l = (int64_t)dl[3 * i];
         uint64_t b2 = 0, e2 = 0;
         if (i + 2 * G < nl) {
             b2 = dl[3 * (i + 2 * G) + 1];
             e2 = dl[3 * (i + 2 * G) + 2];
         }
-#if KMC_CANON_KN
-        if (i + G < nl && e1 - b1 <= (uint64_t)kResKeys) load_keys(p.ent, b1, e1, kn);
-#else
         if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
-#endif
         const uint64_t n = e0 - b0;
         const bool resident = n <= (uint64_t)kResKeys;
         // passes from the list length, capped: repeats do not need passes, and a
@@ -931,25 +802,18 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (n > (uint64_t)kPassDistinct)
             P = (uint32_t)std::min<uint64_t>(kMaxInitPasses, (n + kPassDistinct - 1) / kPassDistinct);
         uint64_t out = b0;  // next free pair of this list's segment
-        PROF_T(t1);
-        PROF_ACC(5, t1 - t0);
         for (uint32_t q = 0; q < P;) {
             uint32_t ncl = 0;
-            PROF_T(ta);
             if (resident) {
-                wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl PROF_PASS);
+                wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl);
             } else {
                 for (uint64_t i0 = b0; i0 < e0; i0 += (uint64_t)kResKeys) {
                     load_keys(p.ent, i0, e0, kr);
-                    wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl PROF_PASS);
+                    wave_insert(kr, q, P, L, wv, p.claim_cap, &L.ovf[par], ncl);
                 }
             }
             if (lane == 0) L.ncl[par][wv] = ncl;
-            PROF_T(tb);
-            PROF_ACC(0, tb - ta);
             lds_barrier();
-            PROF_T(tc0);
-            PROF_ACC(1, tc0 - tb);
             const bool ovf = L.ovf[par] != 0u;
             if (tid == 0) L.ovf[par ^ 1] = 0u;  // last read before this barrier
             if (ovf) {
@@ -984,9 +848,6 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 const uint32_t c = L.tc[sl];
                 L.tk[sl] = kEmptyH;
                 L.tc[sl] = 0u;
-#if KMC_CANON_ABL == 2
-                if (c == 0xFFFFFFF0u)
-#endif
                 {
                     // keys use at most 62 bits (k <= 31): occurrences 1..3 ride in the
                     // top two bits, larger counts escape to pc (K5 reads it only then)
@@ -996,45 +857,16 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 }
             }
             out += total;
-            PROF_T(td);
-            PROF_ACC(2, td - tc0);
             lds_barrier();
-            PROF_T(te);
-            PROF_ACC(3, te - td);
-            PROF_ACC(6, 1ull);
             par ^= 1;
             ++q;
         }
-        PROF_T(tf);
         if (tid == 0) p.ndist[l] = (uint32_t)(out - b0);
-#if KMC_CANON_KN
-#pragma unroll
-        for (int j = 0; j < kRes; ++j) kr[j] = kn[j];
-#endif
         b0 = b1;
         e0 = e1;
         b1 = b2;
         e1 = e2;
-#ifdef KMC_CANON_PROF
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetch, charged here
-#endif
-        PROF_T(tg);
-        PROF_ACC(4, tg - tf);
-        PROF_ACC(7, 1ull);
     }
-#ifdef KMC_CANON_PROF
-    if (lane == 0)
-    {
-        for (int i = 0; i < 8; ++i) atomicAdd(&g_prof[i], pacc[i]);
-        atomicAdd(&g_prof2[0], pp.rounds);
-        atomicAdd(&g_prof2[1], pp.keys);
-        atomicAdd(&g_prof2[2], pp.loops);
-        atomicAdd(&g_prof2[3], pp.cas);
-        atomicAdd(&g_prof2[4], pp.stage);
-        atomicAdd(&g_prof2[5], pp.probe);
-        atomicAdd(&g_prof2[6], pp.qread);
-    }
-#endif
 }
 
 // K4s (round 2): the common list, n <= sort_cap keys with no key repeated more than
@@ -1084,6 +916,11 @@ __device__ __forceinline__ void defer_list(const HParams &p, int64_t l, uint64_t
     p.defer[3 * i + 2] = e;
 }
 
+// The pair format (K4s, K4 -> K5): a canonical key of k <= 31 bases uses at most
+// 62 bits, so occurrences 1..3 ride in its top two bits and larger counts escape
+// to pc.
+static_assert(2 * KMC_CANON_MAX_K <= 62, "pair format: keys must leave the top two bits free");
+
 // emits (h, cnt) at list offset o (the table kernel's pair format)
 __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned long long h, uint32_t cnt) {
     const uint32_t c = cnt - 1u;  // occurrences - 1, as the table kernel stores them
@@ -1094,11 +931,6 @@ __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned
 
 __device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t hi) { return hi ? (w >> 16) : (w & 0xFFFFu); }
 
-// timing-only ablations (results wrong): 1 = no pairwise check / crowded slots,
-// 2 = no scatter either, 3 = no scan either (rank only), 4 = keys loaded, nothing else
-#ifndef KMC_SORT_ABL
-#define KMC_SORT_ABL 0
-#endif
 
 // start of slot sl's keys in sk (after the scan); slot kSortSlots ends at n
 __device__ __forceinline__ uint32_t slot_start(const K4sLds &S, uint32_t sl, uint32_t n) {
@@ -1124,10 +956,6 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
             const uint32_t i = (uint32_t)(j * kSortBlock + tid);
             kh[j] = i < n ? p.ent[b0 + i] : kEmptyH;
         }
-        if (KMC_SORT_ABL >= 4) {
-            if (tid == 0 && kh[0] == 1ull) p.ndist[l] = 0u;  // keeps the loads
-            continue;
-        }
         reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
         reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
         lds_barrier();  // A: counters zero; the previous list is done
@@ -1148,10 +976,6 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
             }
         }
         lds_barrier();  // B: every key ranked
-        if (KMC_SORT_ABL >= 3) {
-            if (tid == 0 && S.sc[rk[0] & 4095u] == 7u) p.ndist[l] = 0u;
-            continue;
-        }
         // scan: thread t owns counter words 8t .. 8t+7 (slots 16t .. 16t+15)
         const uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
         const uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
@@ -1202,7 +1026,7 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
         for (int j = 0; j < kSortRes; ++j) {
             bool alone = false, shared = false;
             uint32_t pos = 0u;
-            if (KMC_SORT_ABL < 2 && (uint32_t)(j * kSortBlock + tid) < n) {
+            if ((uint32_t)(j * kSortBlock + tid) < n) {
                 const uint32_t sl = (uint32_t)kh[j] & (kSortSlots - 1);
                 const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
                 const uint32_t m = slot_start(S, sl + 1u, n) - a;
@@ -1225,10 +1049,6 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
             qn += (uint32_t)__popcll(sm);
         }
         lds_barrier();  // D: the shared keys sorted by slot
-        if (KMC_SORT_ABL >= 1) {
-            if (tid == 0 && S.sk[0] == 1ull) p.ndist[l] = 0u;
-            continue;
-        }
         // the wave's queued keys, 64 at a time: the first occurrence in its slot is
         // emitted with the slot's count of its key
         for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
@@ -1293,13 +1113,10 @@ __global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4)))
 }
 
 // K5: pairs to their final place; record offsets.  Four loads in flight per thread
-// (KMC_PLACE_U; 1 and 8 measured: C4R place 9.4 / 8.1 ms against 8.3, C4 within the
+// (KMC_PLACE_U; 1 and 8 measured, and non-temporal loads / stores: C4R place 9.4 / 8.1 ms against 8.3, C4 within the
 // box noise; four consecutive pairs per thread with 16-byte stores: no gain either).
 #ifndef KMC_PLACE_U
 #define KMC_PLACE_U 4
-#endif
-#ifndef KMC_PLACE_NT
-#define KMC_PLACE_NT 0  // 1: non-temporal pair loads, 2: and output stores (same-box A/B: no gain)
 #endif
 __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
     const int64_t l = blockIdx.x;
@@ -1309,7 +1126,7 @@ __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
 #pragma unroll
         for (int u = 0; u < KMC_PLACE_U; ++u) {
             const uint64_t i = i0 + 256u * u;
-            x[u] = i < m ? (KMC_PLACE_NT ? __builtin_nontemporal_load(p.pk + src + i) : p.pk[src + i]) : 0ull;
+            x[u] = i < m ? p.pk[src + i] : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < KMC_PLACE_U; ++u) {
@@ -1318,13 +1135,8 @@ __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
                 const uint32_t tag = (uint32_t)(x[u] >> 62);
                 const uint64_t key = x[u] & 0x3FFFFFFFFFFFFFFFull;
                 const uint32_t cnt = tag < 3u ? tag + 1u : p.pc[src + i];
-                if (KMC_PLACE_NT >= 2) {
-                    __builtin_nontemporal_store(key, p.out_keys + dst + i);
-                    __builtin_nontemporal_store(cnt, p.out_counts + dst + i);
-                } else {
-                    p.out_keys[dst + i] = key;
-                    p.out_counts[dst + i] = cnt;
-                }
+                p.out_keys[dst + i] = key;
+                p.out_counts[dst + i] = cnt;
             }
         }
     }
@@ -1371,16 +1183,6 @@ extern "C" int kmc_diag_canon_sort_cap(unsigned cap) {
     return KMC_OK;
 }
 
-#ifdef KMC_CANON_PROF
-extern "C" int kmc_diag_canon_prof(unsigned long long *host16) {  // read and reset
-    if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_prof), 64) != hipSuccess ||
-        hipMemcpyFromSymbol(host16 + 8, HIP_SYMBOL(g_prof2), 64) != hipSuccess)
-        return 1;
-    unsigned long long z[8] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, 64) != hipSuccess ||
-           hipMemcpyToSymbol(HIP_SYMBOL(g_prof2), z, 64) != hipSuccess;
-}
-#endif
 
 extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k,
                                         unsigned flags, uint64_t *keys, uint32_t *counts, uint64_t capacity,

@@ -16,8 +16,10 @@ constexpr int64_t kMaxGridY = 32768;
 extern thread_local hipEvent_t t_trace_before, t_trace_after;
 
 // 9 <= k <= KMC_DENSE_MAX_K: radix-partitioned dense counting (kmc_radix.hip).
-// size_only: report the workspace size in *size_out instead of launching.
-int radix_dense(const ::kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out);
+// a->data is 16-byte aligned; ibias is added to every record offset (the caller's
+// misalignment, already added to a's ranges).  size_only: report the workspace size
+// in *size_out instead of launching.
+int radix_dense(const ::kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_only, size_t *size_out);
 
 // splitmix64 output n (0-based) of the stream seeded with `seed` (Steele et al.):
 // z = seed + (n+1)*golden; two xor-shift-multiply rounds; final xor-shift.

@@ -60,7 +60,11 @@ void usage(FILE *f) {
             "  --max-seqs N      the reference's MAX_SEQS cap (default %d, which keeps %d records\n"
             "                    like the reference); 0 = unlimited\n"
             "  --out DIR         directory of parallel_results.csv and sequential_results.csv\n"
-            "                    (default .)\n"
+            "                    (default .).  Both come from the GPU: without --dropin the two files\n"
+            "                    hold the same vector (kmc_pair_distances, exact integer sums, which is\n"
+            "                    what the reference's CPU sequentialKmerCount2 computes), so diffing them\n"
+            "                    checks nothing; with --dropin parallel_results.csv holds minKmeres2_hip's\n"
+            "                    float sums and sequential_results.csv the exact ones (no CPU path here)\n"
             "  --counts FILE     write the histogram: one line per k-mer code, 'kmer<TAB>c_0 .. c_n-1'\n"
             "                    (bin order of permutation(): first base least significant)\n"
             "  --no-distances    step 1 only (no step 2, no CSV)\n"

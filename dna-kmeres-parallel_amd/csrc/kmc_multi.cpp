@@ -12,6 +12,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -49,20 +50,42 @@ namespace {
 
 // Communicators of one device set, created on first use (ncclCommInitAll is a
 // collective setup of its own, far dearer than a 21 MB all-reduce) and kept until
-// kmc_multi_release().
+// kmc_multi_release().  RCCL communicators are not thread-safe, so every entry
+// carries its own mutex, held by a kmc_count_multi call from ncclGroupStart until
+// its copy-back has synchronised: calls on the same device set serialise their
+// collectives, calls on disjoint sets run concurrently.  An entry whose collective
+// failed is dropped (and its communicators aborted), so the next call on that set
+// builds fresh ones instead of reusing a communicator in an error state.
+struct CommSet {
+    std::mutex mu;
+    std::vector<ncclComm_t> comms;
+};
 std::mutex g_comm_mu;
-std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+std::map<std::vector<int>, std::shared_ptr<CommSet>> g_comms;
 
-int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
+int comms_for(const std::vector<int> &devs, std::shared_ptr<CommSet> &out) {
     std::lock_guard<std::mutex> lk(g_comm_mu);
     auto it = g_comms.find(devs);
     if (it == g_comms.end()) {
-        std::vector<ncclComm_t> c(devs.size());
-        if (ncclCommInitAll(c.data(), (int)devs.size(), devs.data()) != ncclSuccess) return KMC_ERR_RCCL;
-        it = g_comms.emplace(devs, std::move(c)).first;
+        auto cs = std::make_shared<CommSet>();
+        cs->comms.resize(devs.size());
+        if (ncclCommInitAll(cs->comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) return KMC_ERR_RCCL;
+        it = g_comms.emplace(devs, std::move(cs)).first;
     }
     out = it->second;
     return KMC_OK;
+}
+
+// Remove a failed set from the cache (if it is still the cached one) and abort its
+// communicators.  The caller holds cs->mu.
+void drop_comms(const std::vector<int> &devs, const std::shared_ptr<CommSet> &cs) {
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        auto it = g_comms.find(devs);
+        if (it != g_comms.end() && it->second == cs) g_comms.erase(it);
+    }
+    for (auto &c : cs->comms) (void)ncclCommAbort(c);
+    cs->comms.clear();
 }
 
 struct DevBufs {
@@ -194,17 +217,33 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     for (auto &d : b)
         if (d.rc) return fail(d.rc);
     // one all-reduce of the int32 matrix (and the invalid vector) over xGMI
-    std::vector<ncclComm_t> comms;
-    rc = comms_for(devs, comms);
+    std::shared_ptr<CommSet> cs;
+    rc = comms_for(devs, cs);
     if (rc) return fail(rc);
+    std::unique_lock<std::mutex> use(cs->mu);  // this set's communicators, until the copy-back is done
+    if (cs->comms.empty()) {                   // dropped by a failed call while we waited: build anew
+        use.unlock();
+        cs.reset();
+        rc = comms_for(devs, cs);
+        if (rc) return fail(rc);
+        use = std::unique_lock<std::mutex>(cs->mu);
+    }
     ncclResult_t nr = ncclGroupStart();
     for (int i = 0; i < ndev && nr == ncclSuccess; ++i) {
-        nr = ncclAllReduce(b[i].sum, b[i].sum, nb * num_seqs, ncclInt32, ncclSum, comms[i], b[i].st);
+        nr = ncclAllReduce(b[i].sum, b[i].sum, nb * num_seqs, ncclInt32, ncclSum, cs->comms[i], b[i].st);
         if (nr == ncclSuccess && invalid)
-            nr = ncclAllReduce(b[i].inv, b[i].inv, num_seqs, ncclInt32, ncclSum, comms[i], b[i].st);
+            nr = ncclAllReduce(b[i].inv, b[i].inv, num_seqs, ncclInt32, ncclSum, cs->comms[i], b[i].st);
     }
     if (nr == ncclSuccess) nr = ncclGroupEnd();
     else ncclGroupEnd();
+    bool comm_ok = nr == ncclSuccess;
+    if (comm_ok) {
+        for (auto &d : b) {  // the collective itself finished on every device
+            (void)hipSetDevice(d.dev);
+            if (hipStreamSynchronize(d.st) != hipSuccess) comm_ok = false;
+        }
+        if (!comm_ok) nr = ncclSystemError;
+    }
     if (nr == ncclSuccess) {
         (void)hipSetDevice(b[0].dev);
         if (hipMemcpyAsync(sum, b[0].sum, sum_bytes, hipMemcpyDeviceToHost, b[0].st) != hipSuccess) nr = ncclSystemError;
@@ -213,15 +252,23 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
             nr = ncclSystemError;
         if (hipStreamSynchronize(b[0].st) != hipSuccess) nr = ncclSystemError;
     }
+    if (!comm_ok) drop_comms(devs, cs);
+    use.unlock();
     release(b);
     (void)hipSetDevice(cur);
     return nr == ncclSuccess ? KMC_OK : KMC_ERR_RCCL;
 }
 
 extern "C" int kmc_multi_release(void) {
-    std::lock_guard<std::mutex> lk(g_comm_mu);
-    for (auto &e : g_comms)
-        for (auto &c : e.second) ncclCommDestroy(c);
-    g_comms.clear();
+    std::map<std::vector<int>, std::shared_ptr<CommSet>> all;
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        all.swap(g_comms);
+    }
+    for (auto &e : all) {
+        std::lock_guard<std::mutex> use(e.second->mu);  // wait for a call still using the set
+        for (auto &c : e.second->comms) ncclCommDestroy(c);
+        e.second->comms.clear();
+    }
     return KMC_OK;
 }

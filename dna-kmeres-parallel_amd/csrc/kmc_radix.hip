@@ -46,13 +46,6 @@
 #ifndef KMC_R4_U
 #define KMC_R4_U 4  // R4 16-byte entry loads in flight per lane (2 / 4 / 8 measured equal, same box)
 #endif
-#ifndef KMC_R4_NT
-#define KMC_R4_NT 0  // 1: R4 reads the entries with non-temporal loads (same-box A/B: no gain)
-#endif
-// tiles per wave in one R3 ring round (more: fewer barriers, more ring overflows)
-#ifndef KMC_RING_PROF
-#define KMC_RING_PROF 0  // diagnostic: per-phase shader-clock cycles of workgroup 0 (printf)
-#endif
 #ifndef KMC_RING_RT
 #define KMC_RING_RT 1
 #endif
@@ -74,8 +67,9 @@ __host__ __device__ constexpr int low_bits(int k) {
 }
 
 struct RParams {
-    const char *data;
+    const char *data;        // 16-byte aligned
     const void *indices;
+    int64_t ibias;           // added to every indices[] value (kmc_stream.h rec_off)
     int64_t n;
     int64_t wl, wh, rl, rh;
     int derive;
@@ -244,10 +238,6 @@ struct RRingOp {
     unsigned long long P0;
     uint32_t f, v;
     int held = 0;          // tiles of this round taken (workgroup-uniform)
-#if KMC_RING_PROF
-    // diagnostic: shader-clock cycles per phase, summed over this wave's rounds
-    unsigned long long t_last = 0, t_sc = 0, t_b1 = 0, t_fl = 0, t_b2 = 0, rounds = 0;
-#endif
 
     __device__ void before_tile() {}
 
@@ -381,24 +371,9 @@ struct RRingOp {
     __device__ void after_iter(int64_t i, int64_t per, bool) {
         if (++held < KMC_RING_RT && i + 1 < per) return;
         held = 0;
-#if KMC_RING_PROF
-        const unsigned long long ta = __builtin_readcyclecounter();
-        if (t_last) t_sc += ta - t_last;
-#endif
         lds_barrier();  // every window of the round is ranked and in its ring
-#if KMC_RING_PROF
-        const unsigned long long tb = __builtin_readcyclecounter();
-#endif
         flush();
-#if KMC_RING_PROF
-        const unsigned long long tc = __builtin_readcyclecounter();
-#endif
         lds_barrier();  // rings read, W set up: the next round may write
-#if KMC_RING_PROF
-        const unsigned long long td = __builtin_readcyclecounter();
-        if (t_last) { t_b1 += tb - ta; t_fl += tc - tb; t_b2 += td - tc; ++rounds; }
-        t_last = td;
-#endif
     }
 
     // end of a piece: the partial segment left in the ring, entry by entry
@@ -460,12 +435,6 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         op.finish();
         __syncthreads();
-#if KMC_RING_PROF
-        if (w == 0 && lane == 0 && op.rounds > 0)
-            printf("ring_prof k=%d wave=%d rec=%lld rounds=%llu scatter=%.0f bar1=%.0f flush=%.0f bar2=%.0f cyc/round\n", K,
-                   wave, (long long)s, op.rounds, (double)op.t_sc / op.rounds, (double)op.t_b1 / op.rounds,
-                   (double)op.t_fl / op.rounds, (double)op.t_b2 / op.rounds);
-#endif
     }
 }
 
@@ -511,15 +480,7 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
         // four 16-byte loads in flight per lane (64 KB per CU): one per iteration
         // left the loop waiting on HBM latency
         uint64_t i = threadIdx.x;
-#if KMC_R4_NT
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        const auto ld = [&](uint64_t k) {
-            const u32x4 y = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(v + k));
-            return make_uint4(y[0], y[1], y[2], y[3]);
-        };
-#else
-        const auto ld = [&](uint64_t k) { return v[k]; };
-#endif
+        const auto ld = [&](uint64_t k) { return v[k]; };  // (non-temporal loads: no gain, same-box A/B)
         for (; i + (KMC_R4_U - 1) * 1024 < nvec; i += KMC_R4_U * 1024) {
             uint4 x[KMC_R4_U];
 #pragma unroll
@@ -725,7 +686,7 @@ struct RCache {
 std::vector<RCache> r_ws;
 
 template <int K>
-int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out) {
+int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_only, size_t *size_out) {
     int device = 0;
     hipError_t he = hipGetDevice(&device);
     if (he != hipSuccess) return (int)he;
@@ -765,6 +726,7 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
     RParams p;
     p.data = a->data;
     p.indices = a->indices;
+    p.ibias = ibias;
     p.n = n;
     p.wl = wl;
     p.wh = wh;
@@ -818,13 +780,13 @@ int run_radix(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *s
 }  // namespace
 
 // Entry used by kmc_dense.hip for 9 <= k <= KMC_DENSE_MAX_K.
-int radix_dense(const kmc_dense_args *a, hipStream_t st, bool size_only, size_t *size_out) {
+int radix_dense(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_only, size_t *size_out) {
     switch (a->k) {
-        case 9: return run_radix<9>(a, st, size_only, size_out);
-        case 10: return run_radix<10>(a, st, size_only, size_out);
-        case 11: return run_radix<11>(a, st, size_only, size_out);
-        case 12: return run_radix<12>(a, st, size_only, size_out);
-        case 13: return run_radix<13>(a, st, size_only, size_out);
+        case 9: return run_radix<9>(a, ibias, st, size_only, size_out);
+        case 10: return run_radix<10>(a, ibias, st, size_only, size_out);
+        case 11: return run_radix<11>(a, ibias, st, size_only, size_out);
+        case 12: return run_radix<12>(a, ibias, st, size_only, size_out);
+        case 13: return run_radix<13>(a, ibias, st, size_only, size_out);
         default: return KMC_ERR_UNSUPPORTED_K;
     }
 }

@@ -25,12 +25,6 @@
 #ifndef KMC_NT
 #define KMC_NT 1
 #endif
-// Diagnostic builds only (scripts/kbench.py): KMC_ABLATE=1 replaces the
-// per-window work by a register XOR (codes still computed), KMC_ABLATE=2 also
-// skips the decode (loads only).  The shipped library is built with KMC_ABLATE=0.
-#ifndef KMC_ABLATE
-#define KMC_ABLATE 0
-#endif
 
 namespace kmc {
 
@@ -151,9 +145,12 @@ struct Geom {
     int64_t T0, T1, tpw;
 };
 
+// Record offset i as a position in p.data: indices[i] + p.ibias (the bias is the
+// misalignment of the caller's data pointer, which the library rounds down to 16
+// bytes: offsets and ranges move up by it, the bytes stay where they are).
 template <class Idx, class P>
 __device__ __forceinline__ int64_t rec_off(const P &p, int64_t i) {
-    return (int64_t)((const Idx *)p.indices)[i];
+    return (int64_t)((const Idx *)p.indices)[i] + p.ibias;
 }
 
 template <class Idx, class P>
@@ -298,12 +295,7 @@ struct TileStream {
             r[SN] = mask_range(r[SN], ((t + 1) << kTileShift) + (int64_t)lane * 16, rl, rh);
         const uint4 r_cur = r[S], r_nxt = r[SN];
         uint32_t c_nxt, v_nxt;
-#if KMC_ABLATE == 2
-        c_nxt = r_nxt.x ^ r_nxt.y ^ r_nxt.z ^ r_nxt.w;
-        v_nxt = 0u;
-#else
         decode16(r_nxt, c_nxt, v_nxt);
-#endif
         // halo: next lane's 16 bases; lane 63 takes lane 0 of the next tile
         uint32_t hc = from_next_lane(c_cur);
         uint32_t hv = from_next_lane(v_cur);
@@ -317,11 +309,7 @@ struct TileStream {
         const int64_t base = t << kTileShift;
         const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
         if (interior && !__any((v_cur | hv) != 0u)) {
-#if KMC_ABLATE == 0
             op.template tile<false>(c_cur, hc, 0xFFFFu);
-#else
-            asm volatile("" ::"v"(c_cur), "v"(hc));
-#endif
         } else {
             // boundary tile or invalid bytes: exact per-window mask
             const int64_t pos = base + (int64_t)lane * 16;
@@ -333,11 +321,7 @@ struct TileStream {
             const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(r_nxt), 0);
             if (lane == 63) b_next = b0;
             const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
-#if KMC_ABLATE == 0
             op.template tile<true>(c_cur, hc, W);
-#else
-            asm volatile("" ::"v"(c_cur), "v"(hc), "v"(W));
-#endif
         }
         c_cur = c_nxt;
         v_cur = v_nxt;
@@ -381,12 +365,7 @@ __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int6
 #pragma unroll
         for (int q = 0; q < TS::PF; ++q) ts.r[q] = load_tile_fast<NT>(ts.rsrc, ts.base_off, t0 + q, lane);
         if (tile_straddles(t0, rl, rh)) ts.r[0] = mask_range(ts.r[0], (t0 << kTileShift) + (int64_t)lane * 16, rl, rh);
-#if KMC_ABLATE == 2
-        ts.c_cur = ts.r[0].x ^ ts.r[0].y;
-        ts.v_cur = 0u;
-#else
         decode16(ts.r[0], ts.c_cur, ts.v_cur);
-#endif
         for (int64_t i = 0; i < n; i += TS::NS) ts.template steps<0>(i, n, per, op);
     }
     for (int64_t i = n; i < per; ++i) op.after_iter(i, per, false);

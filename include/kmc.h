@@ -75,7 +75,10 @@ int kmc_version(void);
  *            (s < num_seqs, code < 4^K) is overwritten
  * k = KMC_DROPIN_K (3, like the reference).  No pattern table (c_perms) is
  * needed: codes are computed arithmetically in the reference's bin order.
- * Uses a library-owned device workspace (allocated on first use per device).
+ * Like the reference's char *data, `data` may point anywhere in a buffer (for
+ * example data + off): the library rounds it down to 16 bytes internally and
+ * biases the offsets (the rounded-down bytes share data's page and are never
+ * counted).  Uses a library-owned device workspace (allocated on first use per device).
  * Asynchronous on `stream` (0 = the null stream); the reference synchronises
  * after the launch (main.cu:291), so should the caller. */
 int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_seqs, int *sum,
@@ -84,7 +87,7 @@ int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_
 /* ------------------------------------------------------------------------ */
 /* k-generic, 64-bit-offset dense counter: the generalisation the reference's CPU
  * path (permutationsCountAll, main.cu:636-646) computes for any k, on the GPU.
- *   data        device pointer, 16-byte aligned, readable for [0, data_bytes)
+ *   data        device pointer (any alignment), readable for [0, data_bytes)
  *   indices     device int64[num_seqs + 1]
  *   k           1 .. KMC_DENSE_MAX_K
  *   sum         device int32[4^k * num_seqs], overwritten (layout above)
@@ -145,7 +148,10 @@ int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, int nshard
  * memory.  devices == NULL -> 0 .. ndev-1 (distinct devices).  Synchronous.
  * One host thread per device streams its shard through pinned staging buffers,
  * so all devices load concurrently.  The RCCL communicators of a device set are
- * created on its first call and reused until kmc_multi_release(). */
+ * created on its first call and reused until kmc_multi_release().  Thread-safe:
+ * concurrent calls on the same device set take turns for the collective (RCCL
+ * communicators are not reentrant), calls on disjoint sets run concurrently, and
+ * a set whose collective failed is rebuilt by the next call. */
 int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes, int k,
                     int ndev, const int *devices, int32_t *sum, int32_t *invalid);
 /* Destroys the communicators cached by kmc_count_multi. */

@@ -196,6 +196,68 @@ def check_c4(torch, kmc, data, idx, k, keys, counts, off, slice_bases=2_000_000)
             "slice": "record 1 bases [%d, %d) as a record == oracle (%d distinct)" % (lo, lo + slice_bases, len(exp))}
 
 
+def c1_line(torch, kmc, dev, iters, recs=4, L=250_000, k=4, cpu_reps=40):
+    """Config C1 (BASELINE configs[0]): 1 Mbase synthetic FASTA (4 records x 250
+    kbase, SURVEY.md §8(d) layout), k = 4 (256 bins), the reference's CPU path.
+    The reference's own permutationsCountAll (oracle/_ref, main.cu:636-646) counts
+    each record on 1 thread and on 16 threads (every thread the whole 1 Mbase
+    workload, `cpu_reps` times, so the sample is long enough to time), beside the
+    GPU call (kmc_count_dense, median of launches), whose result is checked bin for
+    bin against the reference's counts."""
+    import numpy as np
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "oracle"), repo]
+    import bench
+    import oracle
+    seed = 0x5EED0000 + k
+    host = kmc.synth_host(recs, L, seed)
+    idx = kmc.synth_indices(recs, L)
+    d = torch.from_numpy(host).to(dev)
+    di = torch.from_numpy(idx).to(dev)
+    out = torch.empty((1 << (2 * k), recs), dtype=torch.int32, device=dev)
+    inv = torch.empty(recs, dtype=torch.int32, device=dev)
+    args = kmc.dense_args(d, di, k, out, invalid=inv)
+    ws = torch.empty(max(kmc.dense_ex_workspace_size(args), 1), dtype=torch.uint8, device=dev)
+    args = kmc.dense_args(d, di, k, out, invalid=inv, workspace=ws)
+    med, best = timed(torch, lambda: kmc.count_dense_ex(args), max(iters, 20))
+    kmers = recs * (L - k + 1)
+    line = {"config": "C1", "k": k, "records": recs, "bases": recs * L, "s_med": med, "s_min": best,
+            "kmers_per_s": kmers / med, "note": "1 Mbase is launch-bound on the GPU (a few us of work)"}
+    if not oracle.have_ref_cpu():
+        line["cpu_baseline"] = None
+        return line
+    oracle.ref_cpu().ref_build_map(k)
+    recs_host = [host[int(idx[r]):int(idx[r + 1])].copy() for r in range(recs)]  # each ends in its '\0'
+    ref = np.stack([oracle.ref_count_bytes(b, k) for b in recs_host], axis=1)  # [4^k + 1][recs], bin 0 invalid
+    got = out.cpu().numpy()
+    assert (got == ref[1:]).all() and (inv.cpu().numpy() == ref[0]).all(), "C1 GPU counts differ from the reference"
+    line["parity"] = "GPU counts + invalid == the reference's permutationsCountAll, every bin of every record"
+    work = [b for _ in range(cpu_reps) for b in recs_host]
+    res = {}
+    for th in (1, 16):
+        per = [work] * th  # each thread: the whole workload cpu_reps times
+
+        def one(i, out_):
+            out_[i] = sum(int(oracle.ref_count_bytes(b, k).astype(np.int64).sum()) for b in per[i])
+        import threading
+        tot = [0] * th
+        ts = [threading.Thread(target=one, args=(i, tot)) for i in range(th)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        dt = time.perf_counter() - t0
+        res[th] = (sum(tot) / dt, dt, sum(tot))
+    line["cpu_baseline"] = {
+        "value": res[16][0], "unit": "k-mers/s", "cores": 16, "kind": "reference", "value_1thread": res[1][0],
+        "sample": "the whole C1 workload (%d records x %d bases) x %d per thread; 16 threads: %.1f s, 1 thread: "
+                  "%.1f s; the reference's permutationsCountAll (main.cu:636-646) built -O2 from /root/reference; "
+                  "CPU: %s" % (recs, L, cpu_reps, res[16][1], res[1][1], cpu_model())}
+    line["gpu_vs_cpu16"] = line["kmers_per_s"] / res[16][0]
+    return line
+
+
 def timed(torch, fn, iters):
     fn()
     torch.cuda.synchronize()
@@ -212,7 +274,7 @@ def timed(torch, fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c3,c4,c4r")
+    ap.add_argument("--configs", default="c1,c3,c4,c4r")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--gbases-c3", type=float, default=10.0)
     ap.add_argument("--gbases-c4", type=float, default=3.1)
@@ -225,6 +287,8 @@ def main():
     import kmc
     dev = torch.device("cuda:0")
     cfgs = a.configs.split(",")
+    if "c1" in cfgs:
+        print(json.dumps(c1_line(torch, kmc, dev, a.iters)), flush=True)
     if "c3r" in cfgs:  # k = 13 over the repeat-rich genome, uppercased (skewed buckets: the rings' cold path)
         import genome_synth
         data, idx, lens, st = genome_synth.repeat_genome(torch, dev, a.gbases_c4)

@@ -28,11 +28,15 @@ def test_argument_errors_need_no_device(kmc):
     assert L.kmc_count_dense(None, None, 0, 0, 3, None, None, None, 0, None) == 0
     assert L.sumKmereCoincidencesGlobalMemory_hip(None, None, 0, None, None) == 0
     assert L.sumKmereCoincidencesGlobalMemory_hip(None, None, 3, None, None) == 1001
-    # misaligned data pointer is refused before any launch
+    # the canonical counter still needs a 16-byte aligned data pointer: refused
+    # before any device call (the dense entry points take any pointer, like
+    # kernels.h:113: tests/test_dense_gpu.py runs them on data + 1 .. 15)
     buf = (ctypes.c_char * 64)()
     base = ctypes.addressof(buf)
     mis = ctypes.c_void_p(base + (1 if base % 16 == 0 else 0) + (16 - base % 16) % 16)
-    assert L.sumKmereCoincidencesGlobalMemory_hip(mis, ctypes.c_void_p(base), 1, ctypes.c_void_p(base), None) == 1003
+    nd = ctypes.c_uint64(0)
+    assert L.kmc_count_canonical_hash(mis, ctypes.c_void_p(base), 1, 21, 0, None, None, 0, ctypes.c_void_p(base),
+                                      ctypes.byref(nd), None) == 1003
 
 
 def test_synth_indices_and_host_generator(kmc):

@@ -101,6 +101,59 @@ def test_dropin_matches_reference_kernel(kmc, oracle, cuda):
         np.testing.assert_array_equal(ours.cpu().numpy(), ref.cpu().numpy())
 
 
+def test_dropin_unaligned_data_matches_reference_kernel(kmc, oracle, cuda):
+    """kernels.h:113 takes any char *data: the drop-in on data + 1 .. 15 (a pointer
+    inside a buffer) against the reference kernel on the same pointer."""
+    import torch
+    if not oracle.have_ref_kernel():
+        pytest.skip("oracle/_ref/libref_kernel.so not built")
+    L = oracle.ref_kernel()
+    assert L.ref_kernel_upload_patterns() == 0
+    rng = np.random.default_rng(33)
+    data, idx = random_records(rng, [3000, 1, 5, 17, 1500, 4099], 0.01, 0.01, 0.002)
+    idx32 = idx.astype(np.int32)
+    n = idx.size - 1
+    di = dev(idx32, cuda)
+    for off in range(16):
+        big = torch.full((data.size + 48,), ord("A"), dtype=torch.uint8, device=cuda)
+        big[off:off + data.size] = dev(data, cuda)
+        d = big[off:]
+        assert d.data_ptr() % 16 == off % 16 or big.data_ptr() % 16 != 0
+        ref = torch.zeros(64 * n, dtype=torch.int32, device=cuda)
+        assert L.ref_kernel_launch(d.data_ptr(), di.data_ptr(), n, ref.data_ptr()) == 0
+        ours = kmc.dropin_count(d, di, n)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(ours.cpu().numpy(), ref.cpu().numpy(), err_msg="offset %d" % off)
+
+
+@pytest.mark.parametrize("k", [3, 8, 11])
+def test_dense_unaligned_data_vs_oracle(kmc, oracle, cuda, k):
+    """kmc_count_dense / kmc_count_dense_ex with a data pointer at every offset mod 16
+    (the library aligns it down and biases the offsets), including a byte-range
+    shard of the offset buffer."""
+    import torch
+    rng = np.random.default_rng(5000 + k)
+    data, idx = random_records(rng, [0, 5, 4096 * 2 + 3, 1, 70_001, 333], 0.003, 0.003, 0.001)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    di = dev(idx, cuda)
+    for off in (1, 7, 8, 15):
+        big = torch.zeros(data.size + 48, dtype=torch.uint8, device=cuda)
+        big[off:off + data.size] = dev(data, cuda)
+        d = big[off:off + data.size]
+        out, inv = kmc.count_dense(d, di, k, data_bytes=data.size, invalid=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), exp, err_msg="offset %d" % off)
+        np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv, err_msg="offset %d" % off)
+        # two shards of the offset buffer sum to the whole
+        acc = np.zeros_like(exp)
+        for (a, b, rl, rh) in kmc.plan_shards(idx, k, 2, 4096):
+            o = torch.empty((1 << (2 * k), idx.size - 1), dtype=torch.int32, device=cuda)
+            kmc.count_dense_ex(kmc.dense_args(d, di, k, o.view(-1), read=(rl, rh), win=(a, b)))
+            torch.cuda.synchronize()
+            acc += o.cpu().numpy()
+        np.testing.assert_array_equal(acc, exp, err_msg="shards, offset %d" % off)
+
+
 @pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_dense_random_vs_oracle(kmc, oracle, cuda, k):
     rng = np.random.default_rng(1000 + k)

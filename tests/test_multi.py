@@ -256,3 +256,53 @@ def test_bench_host_histogram_matches_oracle(oracle):
     for k in (1, 5, 8):
         exp, _ = oracle.count_dense(np.append(b, np.uint8(0)), np.array([0, b.size + 1], dtype=np.int64), k)
         np.testing.assert_array_equal(bench.host_kmer_hist(b, k), exp[:, 0])
+
+
+def _finalize_worker(rank, world, port, q):
+    """bench.finalize (everything after the timed region) at world 2 with gloo on
+    CPU tensors: the N > 1 line must carry the all-reduce time, the node roofline
+    fraction, the RCCL world size and backend, and the reference CPU path on rank 0."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    sys.path[:0] = [repo, os.path.join(repo, "dna-kmeres-parallel_amd"), os.path.join(repo, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import kmc
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    k, L, records = 8, 200_000, 4
+    args = bench.parse(["--gpus", str(world), "--steps", "5", "--cpu-sample", "30000", "--cpu-threads", "2",
+                        "--allreduce-reps", "3", "--k", str(k), "--records", str(records), "--record-len", str(L)])
+    plan = bench.rank_plan("strong", world, rank, records, L, k)
+    base, hold_hi = plan["hold"]
+    data = torch.from_numpy(kmc.synth_host_range(base, hold_hi, L, bench.SEED_BASE + k).copy())
+    matrix = torch.zeros((1 << (2 * k), records), dtype=torch.int32)
+    win = plan["win"]
+    alg = (win[1] - win[0]) + 4 * (1 << (2 * k)) * records
+    kern_ms = 0.5 + rank  # rank 1 is the slow one
+    res = bench.finalize(args, world, rank, "gloo", data, matrix, L, k, records, win, 0.01 * (1 + rank), kern_ms,
+                         alg, timer="host")
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_line_fields():
+    res = dict(_spawn(_finalize_worker, 2))
+    assert res[1] is None
+    r = res[0]
+    assert r["n_gpus"] == 2 and r["config"]["rccl_world"] == 2 and r["config"]["backend"] == "gloo"
+    # max over ranks: rank 1's elapsed and kernel time
+    assert abs(r["ms_per_step"] - 0.02 / 5 * 1e3) < 1e-9 and r["roofline"]["kernel_ms"] == 1.5
+    rf = r["roofline"]
+    for key in ("achieved", "frac", "node_achieved", "node_frac", "node_peak", "alg_bytes_per_kmer"):
+        assert rf[key] > 0, key
+    assert rf["node_peak"] == 2 * rf["peak"]
+    # node fraction = value x algorithmic bytes per k-mer / (N x peak)
+    assert abs(rf["node_frac"] - r["value"] * rf["alg_bytes_per_kmer"] / 1e9 / (2 * rf["peak"])) < 1e-12
+    assert r["allreduce"]["ms"] > 0 and r["allreduce"]["bytes"] == 4 * 65536 * 4
+    cb = r["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] in ("reference", "port")
