@@ -328,26 +328,6 @@ struct TileStream {
         op.after_iter(i, per, true);
     }
 
-    // a run starting at tile t0_: the first PF tiles in flight, tile t0_ decoded
-    __device__ __forceinline__ void start(const char *__restrict__ d, int64_t t0_, int64_t ps_, int64_t pe_,
-                                          int64_t rl_, int64_t rh_, int lane_) {
-        data = d;
-        t0 = t0_;
-        ps = ps_;
-        pe = pe_;
-        rl = rl_;
-        rh = rh_;
-        lane = lane_;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) r[q] = make_uint4(0u, 0u, 0u, 0u);
-        base_off = tile_base(t0, rl);
-        rsrc = tile_rsrc(data, base_off, rh);
-#pragma unroll
-        for (int q = 0; q < PF; ++q) r[q] = load_tile_fast<NT>(rsrc, base_off, t0 + q, lane);
-        if (tile_straddles(t0, rl, rh)) r[0] = mask_range(r[0], (t0 << kTileShift) + (int64_t)lane * 16, rl, rh);
-        decode16(r[0], c_cur, v_cur);
-    }
-
     // steps i .. i+NS-1, stopping at n (the wave's tile count)
     template <int S, class Op>
     __device__ __forceinline__ void steps(int64_t i, int64_t n, int64_t per, Op &op) {
@@ -371,7 +351,21 @@ __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int6
     const int64_t n = t1 > t0 ? t1 - t0 : 0;  // <= per
     if (n > 0) {
         TS ts;
-        ts.start(data, t0, ps, pe, rl, rh, lane);
+        ts.data = data;
+        ts.t0 = t0;
+        ts.ps = ps;
+        ts.pe = pe;
+        ts.rl = rl;
+        ts.rh = rh;
+        ts.lane = lane;
+#pragma unroll
+        for (int q = 0; q < TS::NS; ++q) ts.r[q] = make_uint4(0u, 0u, 0u, 0u);
+        ts.base_off = tile_base(t0, rl);
+        ts.rsrc = tile_rsrc(data, ts.base_off, rh);
+#pragma unroll
+        for (int q = 0; q < TS::PF; ++q) ts.r[q] = load_tile_fast<NT>(ts.rsrc, ts.base_off, t0 + q, lane);
+        if (tile_straddles(t0, rl, rh)) ts.r[0] = mask_range(ts.r[0], (t0 << kTileShift) + (int64_t)lane * 16, rl, rh);
+        decode16(ts.r[0], ts.c_cur, ts.v_cur);
         for (int64_t i = 0; i < n; i += TS::NS) ts.template steps<0>(i, n, per, op);
     }
     for (int64_t i = n; i < per; ++i) op.after_iter(i, per, false);

@@ -307,61 +307,6 @@ def test_k8_hot_half_scans_with_fallback(kmc, oracle, cuda):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
-@pytest.fixture
-def steal_hook(kmc):
-    """kmc_diag_dense_steal(steal, owner_delay_ticks): thieves on/off, owners of
-    every third home range delayed (100 MHz ticks); restored afterwards."""
-    hook = kmc.lib().kmc_diag_dense_steal
-    yield hook
-    assert hook(-1, 0) == 0
-
-
-@pytest.mark.parametrize("k", [3, 7, 8])
-@pytest.mark.parametrize("mode", ["late_owners", "no_thieves"])
-def test_dense_work_stealing_vs_oracle(kmc, oracle, cuda, steal_hook, k, mode):
-    """The dense kernel's dynamic work split: owners claim their first / last
-    pieces chunk by chunk, thieves take chunks from the back.  With every third
-    owner held back 300 us its pieces are counted by thieves (victims not yet
-    started, thief slab slots, whole records stolen); with thieves off the owners
-    claim everything.  Multi-MB records cut by many home ranges, short records,
-    invalid bytes, and a byte-range shard; bit-exact against the oracle."""
-    import torch
-    assert steal_hook(1, 30_000) == 0 if mode == "late_owners" else steal_hook(0, 0) == 0
-    rng = np.random.default_rng(6100 + k)
-    lens = [9_000_003, 3, 17, 250_000, 31_000_000, 1, 4096 * 5 + 11, 6_000_000] + [int(x) for x in rng.integers(0, 5000, 40)]
-    data, idx = random_records(rng, lens, 0.002, 0.002, 0.0005)
-    got, inv = run_dense(kmc, cuda, data, idx, k)
-    exp, exp_inv = oracle.count_dense(data, idx, k)
-    np.testing.assert_array_equal(got, exp)
-    np.testing.assert_array_equal(inv, exp_inv)
-    # a shard (window range + halo) of the same buffer
-    a, b = 5_000_000, 40_000_000
-    d, di = dev(data, cuda), dev(idx, cuda)
-    out = torch.full((1 << (2 * k), idx.size - 1), -7, dtype=torch.int32, device=cuda)
-    kmc.count_dense_ex(kmc.dense_args(d, di, k, out, read=(a, b + k - 1), win=(a, b)))
-    torch.cuda.synchronize()
-    ref, _ = oracle.count_dense(data, idx, k, win=(a, b))
-    np.testing.assert_array_equal(out.cpu().numpy(), ref)
-
-
-def test_k8_wraps_with_stolen_pieces(kmc, oracle, cuda, steal_hook):
-    """k = 8 wrap detection and the record recount when thieves hold pieces of the
-    wrapping records (late owners): poly-A records and hot (65 % A) records."""
-    assert steal_hook(1, 30_000) == 0
-    rng = np.random.default_rng(8080)
-    acgt = np.frombuffer(b"ACGT", np.uint8)
-    hot = np.where(rng.random(40 << 20) < 0.65, ord("A"), acgt[rng.integers(1, 4, 40 << 20)]).astype(np.uint8)
-    seqs = [hot, np.full(6 << 20, ord("A"), np.uint8), acgt[rng.integers(0, 4, 8 << 20)],
-            np.full(100_000, ord("A"), np.uint8)]
-    recs = [np.append(x, np.uint8(0)) for x in seqs]
-    data = np.concatenate(recs)
-    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
-    got, inv = run_dense(kmc, cuda, data, idx, 8)
-    exp, exp_inv = oracle.count_dense(data, idx, 8)
-    np.testing.assert_array_equal(got, exp)
-    np.testing.assert_array_equal(inv, exp_inv)
-
-
 @pytest.mark.parametrize("k", [4, 8])
 def test_range_shards_sum_to_full(kmc, oracle, cuda, k):
     """kmc_count_dense_ex over disjoint window ranges, each reading only its
