@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -659,6 +660,8 @@ void *kernel_ptr() {
     return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, Cfg<K>::HM, Idx, Cfg<K>::BLOCK>);
 }
 
+// CUs left out of the dense grid (kmc_set_reserved_cus)
+std::atomic<int> g_reserved_cus{0};
 
 template <int K, class Idx>
 int grid_size(int device, int &G) {
@@ -679,7 +682,9 @@ int grid_size(int device, int &G) {
         if (e != hipSuccess) return (int)e;
         d.occ[K][ix] = nb > 0 ? nb : 1;
     }
-    G = d.cus * d.occ[K][ix];
+    // kmc_set_reserved_cus: leave that many CUs to a concurrent kernel
+    const int cus = d.cus - g_reserved_cus.load(std::memory_order_relaxed);
+    G = (cus > 0 ? cus : 1) * d.occ[K][ix];
     return 0;
 }
 
@@ -940,6 +945,12 @@ size_t workspace_for(int k, int device, bool derive, int64_t wl, int64_t wh) {
 }  // namespace kmc
 
 using namespace kmc;
+
+extern "C" int kmc_set_reserved_cus(int n) {
+    if (n < 0 || n > 64) return KMC_ERR_INVALID_ARG;
+    g_reserved_cus.store(n, std::memory_order_relaxed);
+    return KMC_OK;
+}
 
 extern "C" int kmc_trace_set_events(hipEvent_t before, hipEvent_t after) {
     t_trace_before = before;

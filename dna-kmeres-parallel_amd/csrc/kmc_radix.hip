@@ -16,12 +16,23 @@
 //               stage[s][b*2^LOW + c] (record-major, coalesced)
 //   R5 place    transpose stage into sum[s + ld*code] (k-mer-major, coalesced)
 //
-// LOW = min(2k - 6, 15), 16 from k = 12 on (low_bits).  Bytes per k-mer: 1 (R1) +
-// 1 (R3) input, 2 written + 2 read entries, plus the output twice; the LDS
-// histograms see the same bank-conflict-bound atomic rate as the k <= 8 kernels.
+// Sampled mode (large inputs: >= 4096 windows per (record, bucket, workgroup) on
+// average, e.g. C3): R1's full read of the input is replaced by a 1-in-8 tile sample
+// (S1, the same kernel with sample_tiles) whose weighted counts size one region
+// per (s, b, w) with a margin (radix_cap_kernel); R2 scans the capacities, R3
+// writes into the regions and records each one's fill in cnt, R4 walks a list as
+// its G regions.  A region that overflows (or capacities beyond the entry array)
+// raises a flag, and the exact R1 + R2 + R3, launched behind it and gated on it,
+// rerun on the device -- no host sync, exact either way.
+//
+// LOW = min(2k - 6, 15), 16 from k = 12 on (low_bits).  Bytes per k-mer: 1 (R1;
+// 1/8 sampled) + 1 (R3) input, 2 written + 2 read entries, plus the output twice;
+// the LDS histograms see the same bank-conflict-bound atomic rate as the k <= 8
+// kernels.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <mutex>
 #include <vector>
@@ -75,14 +86,28 @@ struct RParams {
     int derive;
     int G;           // workgroups of R1/R3
     int nbk;         // buckets per record
-    uint32_t *cnt;   // [n][nbk][G]
-    uint64_t *off;   // [n*nbk*G + 1] exclusive prefix of cnt
+    uint32_t *cnt;   // [n][nbk][G] entries of list (s, b) from workgroup w
+    uint64_t *off;   // [n*nbk*G + 1] start of each (s, b, w) region of ent
     uint16_t *ent;   // entries
     uint32_t *stage; // [n][4^k]
     int32_t *sum;
     int64_t ld;
     int32_t *invalid;
+    // sampled mode (radix_count_kernel<SAMPLE>): regions sized from a 1-in-8 tile sample
+    uint32_t *capv;      // [n][nbk][G] region capacities (multiples of 32); null: exact offsets
+    uint32_t *flag;      // overflow lists full (or capacities beyond ent_cap): exact rerun
+    const uint32_t *gate;  // non-null: the kernel runs only if *gate != 0 (the exact rerun)
+    uint64_t ent_cap;    // entries ent holds
+    unsigned long long *ovf;  // [G][ovf_cap] entries past their region, as stage indices
+    uint32_t *ovf_cnt;   // [G]
+    uint32_t ovf_cap;
+    float cap_scale;     // test hook: capacities scaled (< 1 forces overflows)
 };
+
+// A launch of the exact rerun returns at once unless the sampled pass overflowed.
+__device__ __forceinline__ bool gated_off(const RParams &p) {
+    return p.gate != nullptr && __hip_atomic_load(p.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+}
 
 // R1 op: bucket counters with kCountRep replicas interleaved (counter b of lane l
 // at word b*kCountRep + l % kCountRep), so the 32 lanes of an LDS lane group
@@ -92,6 +117,7 @@ template <int K>
 struct RCountOp {
     static constexpr int LOW = low_bits(K);
     uint32_t *c;  // LDS bucket counters (this lane's replica)
+    uint32_t wgt;  // added per window (the sampled walk: its tile stride)
     __device__ void before_tile() {}
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
@@ -99,16 +125,58 @@ struct RCountOp {
         for (int j = 0; j < 16; ++j) {
             const uint32_t code = window_code_rt<K>(lo, hi, j);
             if (!MASKED || ((W >> j) & 1u))
-                __hip_atomic_fetch_add(&c[(code >> LOW) * kCountRep], 1u, __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&c[(code >> LOW) * kCountRep], wgt, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __device__ void after_iter(int64_t, int64_t, bool) {}
 };
 
+// The sampled walk of a wave run [a0, a1): one tile in kSampleStride (a pseudo-random
+// phase per run; every tile of runs up to kSampleAll tiles), each window counted
+// with weight = the stride, kSampleFlight tiles in flight.  A sampled tile has no next tile:
+// the windows of lane 63 that need its halo are skipped (1.2 % of them at k = 13),
+// which the capacities' margin covers.
+constexpr int kSampleStride = 8, kSampleAll = 16, kSampleFlight = 8;
+template <int K, class Op>
+__device__ __forceinline__ void sample_tiles(const char *__restrict__ data, int64_t a0, int64_t a1, int64_t ps,
+                                             int64_t pe, int64_t rl, int64_t rh, int lane, uint32_t seed, Op &op) {
+    const int64_t len = a1 - a0;
+    if (len <= 0) return;
+    const int stride = len <= kSampleAll ? 1 : kSampleStride;
+    op.wgt = (uint32_t)stride;
+    const int64_t phase = stride == 1 ? 0 : (int64_t)((seed * 0x9E3779B1u) >> 29);
+    for (int64_t t = a0 + phase; t < a1; t += kSampleFlight * stride) {
+        uint4 r[kSampleFlight];
+#pragma unroll
+        for (int u = 0; u < kSampleFlight; ++u) {
+            const int64_t tt = t + (int64_t)u * stride;
+            r[u] = tt < a1 ? load_lane(data, tt, lane, rl, rh) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kSampleFlight; ++u) {
+            const int64_t tt = t + (int64_t)u * stride;
+            if (tt >= a1) break;  // wave-uniform
+            uint32_t code, bad;
+            decode16(r[u], code, bad);
+            const uint32_t hc = from_next_lane(code);
+            const uint32_t b_own = bad_mask16(r[u]);
+            uint32_t b_next = from_next_lane(b_own);
+            if (lane == 63) b_next = 0xFFFFu;  // no halo: its windows across the tile end are skipped
+            const int64_t pos = (tt << kTileShift) + (int64_t)lane * 16;
+            const int64_t dlo = ps - pos, dhi = pe - pos;
+            const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
+            const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
+            const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
+            op.template tile<true>(code, hc, W);
+        }
+    }
+}
+
 // R1: the piece walk of the dense kernel, counting per record piece the windows
-// of each bucket in LDS -> cnt[(s*NBK + b)*G + w].
-template <int K, class Idx>
+// of each bucket in LDS -> cnt[(s*NBK + b)*G + w].  SAMPLE: the sampled walk
+// (sample_tiles), whose weighted counts estimate the same numbers.
+template <int K, class Idx, bool SAMPLE = false>
 __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
     constexpr int BLOCK = 1024;
     constexpr int NWAVES = BLOCK / 64;
@@ -119,6 +187,7 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int w = blockIdx.x;
+    if (gated_off(p)) return;
     const Geom g = make_geom<Idx>(p);
     const int64_t tb = g.T0 + (int64_t)w * g.tpw;
     const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
@@ -142,8 +211,12 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
         const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-        RCountOp<K> op{s_cnt + (lane & (kCountRep - 1))};
-        stream_tiles<K, RCountOp<K>, KMC_RCOUNT_PF, KMC_RCOUNT_NT>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        RCountOp<K> op{s_cnt + (lane & (kCountRep - 1)), 1u};
+        if constexpr (SAMPLE) {
+            sample_tiles<K>(p.data, a0, a1, ps, pe, g.rl, g.rh, lane, (uint32_t)(w * 16 + wave) ^ (uint32_t)s, op);
+        } else {
+            stream_tiles<K, RCountOp<K>, KMC_RCOUNT_PF, KMC_RCOUNT_NT>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        }
         __syncthreads();
         for (int b = tid; b < NBK; b += BLOCK) {
             const uint4 *r4 = reinterpret_cast<const uint4 *>(s_cnt + b * kCountRep);
@@ -156,6 +229,37 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
             p.cnt[lbase + (int64_t)b * p.G] = t;
         }
         __syncthreads();
+    }
+}
+
+// Sampled mode: the region capacity of every (s, b, w) from the weighted sample
+// count c (an estimate of the region's entries): 1.05 c + 6 sigma + 64, sigma =
+// sqrt(8 c) the Poisson error of a 1-in-8 sample, rounded up to 32 entries (whole
+// 64-byte segments: regions stay segment-aligned) and at most the piece's windows;
+// 0 where workgroup w holds no piece of record s (whatever cnt held there).  Clears
+// cnt: R3 writes the fills, an exact rerun's R1 the counts.
+template <int K, class Idx>
+__global__ __launch_bounds__(256) void radix_cap_kernel(RParams p) {
+    const int64_t m = p.n * p.nbk * p.G;
+    const Geom g = make_geom<Idx>(p);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (int64_t)gridDim.x * 256) {
+        const int64_t w = i % p.G, s = i / ((int64_t)p.nbk * p.G);
+        const int64_t tb = g.T0 + w * g.tpw;
+        const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
+        int64_t ca, ce;
+        record_windows<K, Idx>(p, g, s, ca, ce);
+        const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
+        const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
+        const int64_t ps = ca > R0 ? ca : R0, pe = ce < R1 ? ce : R1;
+        uint32_t cap = 0u;
+        if (tb < te && ps < pe) {
+            const float c = (float)p.cnt[i];
+            const float x = (1.05f * c + 6.0f * sqrtf(8.0f * c) + 64.0f) * p.cap_scale;
+            const int64_t pmax = (pe - ps + 31) & ~(int64_t)31;
+            cap = x >= (float)pmax ? (uint32_t)pmax : (((uint32_t)x + 31u) & ~31u);
+        }
+        p.capv[i] = cap;
+        p.cnt[i] = 0u;
     }
 }
 
@@ -228,6 +332,7 @@ struct RRingOp {
     uint16_t *ring;        // LDS, NBK * RING entries
     uint32_t *W;           // LDS, [2][NBK]
     unsigned long long *gH;  // LDS, [NBK]: list index of every bucket's ring slot 0 this round
+    unsigned long long *lim;  // LDS, [NBK]: end of the bucket's region (sampled mode; else ~0)
     uint16_t *dummy;       // LDS, 2 halfwords per lane
     uint16_t *ent;
     int tid, lane;
@@ -237,9 +342,35 @@ struct RRingOp {
     // f = next entry, v = first entry still to be written from the ring
     unsigned long long P0;
     uint32_t f, v;
+    uint32_t f0;           // f at the piece start (the piece's entries: f - f0)
+    uint32_t cap;          // end of the region (relative to P0; ~0: exact offsets)
     int held = 0;          // tiles of this round taken (workgroup-uniform)
+    // sampled mode: this workgroup's overflow list and its LDS counter; stage index
+    // of the piece's record
+    unsigned long long *ovf;
+    uint32_t *ovf_n;
+    uint32_t ovf_cap;
+    unsigned long long sbase;
 
     __device__ void before_tile() {}
+
+    // an entry e of bucket b past its region -> the overflow list (added into stage
+    // by radix_overflow_kernel after R4; a full list raises the exact rerun).  Out of
+    // line, like ovf_seg: cold paths, kept out of the hot loop's code and registers.
+    __device__ __noinline__ void ovf_put(uint32_t b, uint32_t e) const {
+        const uint32_t i = atomicAdd(ovf_n, 1u);
+        if (i < ovf_cap) ovf[i] = sbase + ((unsigned long long)b << RG::LOW) + e;
+    }
+    // this lane's 8 entries (x) of a complete segment past its region, whose ring
+    // LDS address is a & ~63
+    __device__ __noinline__ void ovf_seg(uint32_t a, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) const {
+        const uint32_t bt = ((a & ~63u) - (uint32_t)(uintptr_t)ring) / (2u * RG::RING);
+        const uint32_t i8 = atomicAdd(ovf_n, 8u);
+        const uint32_t w4[4] = {x0, x1, x2, x3};
+        for (uint32_t e = 0; e < 8; ++e)
+            if (i8 + e < ovf_cap)
+                ovf[i8 + e] = sbase + ((unsigned long long)bt << RG::LOW) + ((w4[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+    }
 
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t l, uint32_t h, uint32_t Wm) {
@@ -286,7 +417,13 @@ struct RRingOp {
             for (int j = 0; j < 16; ++j) {
                 const uint32_t lo = (old[j] & 0xFFFFu) >> 1;
                 if ((!MASKED || ((Wm >> j) & 1u)) && lo >= (uint32_t)RG::RING)
-                    ent[gH[(c[j] >> RG::LOW) & (RG::NBK - 1)] + lo] = (uint16_t)(c[j] & ((1u << RG::LOW) - 1u));
+                {
+                    const uint32_t bj = (c[j] >> RG::LOW) & (RG::NBK - 1);
+                    const unsigned long long at = gH[bj] + lo;
+                    const uint32_t e = c[j] & ((1u << RG::LOW) - 1u);
+                    if (at < lim[bj]) ent[at] = (uint16_t)e;
+                    else ovf_put(bj, e);
+                }
             }
         }
     }
@@ -297,12 +434,16 @@ struct RRingOp {
     }
 
     // start of a piece: list (s, b)'s segment of this workgroup begins at F
-    __device__ __forceinline__ void begin(uint32_t b, unsigned long long F, bool owner) {
+    // (sampled mode: F is 32-aligned and the region holds capb entries; entries past
+    // it are dropped and reported by finish())
+    __device__ __forceinline__ void begin(uint32_t b, unsigned long long F, uint32_t capb, bool owner) {
         P0 = F & ~31ull;
-        f = v = (uint32_t)(F - P0);
+        f = v = f0 = (uint32_t)(F - P0);
+        cap = capb == ~0u ? ~0u : f0 + capb;
         if (owner) {
             W[b] = ring_word<K>(b, f);
             gH[b] = P0;
+            lim[b] = capb == ~0u ? ~0ull : P0 + cap;
         }
     }
 
@@ -333,15 +474,21 @@ struct RRingOp {
         uint32_t i0 = j;
         if (h < v && j == 0 && nseg > 0) {  // segment 0 partly before v (piece start, after an overflow)
             for (uint32_t q = 0; q < 32; ++q)
-                if (h + q >= v) ent[P0 + h + q] = ring_entry(b, h, h + q);
+                if (h + q >= v) {
+                    const uint16_t e = ring_entry(b, h, h + q);
+                    if (h + q < cap) ent[P0 + h + q] = e;
+                    else ovf_put(b, e);
+                }
             i0 = j + RG::TPB;
         }
         const uint32_t q = (uint32_t)lane & 3u;
         const uint32_t rowb = (uint32_t)(uintptr_t)row;                      // LDS byte address of the ring
         const uint32_t gs = (uint32_t)((P0 + h) >> 5);                        // list index / 32 of slot 0
         for (uint32_t i = i0; __any(i < nseg); i += RG::TPB) {  // mostly once: two segments are rare
-            // bit 2: a segment to store; bits 0-1: the chunk swizzle
-            const uint32_t A = (rowb + 64u * (i ^ (x8 >> 2))) | (x8 & 3u) | (i < nseg ? 4u : 0u);
+            // bit 2: a segment to store, bit 3: one past its region (to the overflow
+            // list); bits 0-1: the chunk swizzle
+            const bool in = h + 32u * i + 32u <= cap;
+            const uint32_t A = (rowb + 64u * (i ^ (x8 >> 2))) | (x8 & 3u) | (i < nseg ? (in ? 4u : 8u) : 0u);
             uint32_t a[4], g[4];
             quad_bcast4(A, a);
             quad_bcast4(gs + i, g);
@@ -351,6 +498,10 @@ struct RRingOp {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (a[t] & 4u) reinterpret_cast<u32x4 *>(ent + 32ull * g[t])[q] = val[t];
+            if (__builtin_expect(__any(((a[0] | a[1] | a[2] | a[3]) & 8u) != 0u), 0)) {
+                for (int t = 0; t < 4; ++t)  // this lane's 8 entries of the quad's segment t
+                    if (a[t] & 8u) ovf_seg(a[t], val[t][0], val[t][1], val[t][2], val[t][3]);
+            }
         }
         if (fill > (uint32_t)RG::RING) {
             v = f1;  // [h + RING, f1) went straight to the list
@@ -376,12 +527,19 @@ struct RRingOp {
         lds_barrier();  // rings read, W set up: the next round may write
     }
 
-    // end of a piece: the partial segment left in the ring, entry by entry
-    __device__ __forceinline__ void finish() {
+    // end of a piece: the partial segment left in the ring, entry by entry (past the
+    // region: to the overflow list); the piece's entries of the bucket -> *cnt_out
+    // (sampled mode: R4 reads min(cnt, capacity) of them from the region)
+    __device__ __forceinline__ void finish(uint32_t *cnt_out) {
         const uint32_t b = (uint32_t)tid / RG::TPB, j = (uint32_t)tid % RG::TPB;
         const uint32_t h = f & ~31u;
         const uint32_t lo = h > v ? h : v;
-        for (uint32_t g = lo + j; g < f; g += RG::TPB) ent[P0 + g] = ring_entry(b, h, g);
+        for (uint32_t g = lo + j; g < f; g += RG::TPB) {
+            const uint16_t e = ring_entry(b, h, g);
+            if (g < cap) ent[P0 + g] = e;
+            else ovf_put(b, e);
+        }
+        if (j == 0) *cnt_out = f - f0;
     }
 };
 
@@ -394,10 +552,18 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[RG::NBK * RG::RING];
     __shared__ uint32_t s_W[2 * RG::NBK];
     __shared__ unsigned long long s_gH[RG::NBK];
+    __shared__ unsigned long long s_lim[RG::NBK];
     __shared__ uint16_t s_dummy[128];
     __shared__ int64_t s_first;
+    __shared__ uint32_t s_ovf_n;
 
     const int tid = threadIdx.x, lane = tid & 63;
+    if (gated_off(p)) return;
+    // sampled mode: the capacities must fit the entry array (else the exact rerun)
+    if (p.capv != nullptr && p.off[p.n * RG::NBK * p.G] > p.ent_cap) {
+        if (tid == 0) __hip_atomic_store(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int w = blockIdx.x;
     const Geom g = make_geom<Idx>(p);
@@ -406,7 +572,10 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
     if (tb >= te) return;
     const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
     const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
-    if (tid == 0) s_first = first_record_at<Idx>(p, R0);
+    if (tid == 0) {
+        s_first = first_record_at<Idx>(p, R0);
+        s_ovf_n = 0u;
+    }
     __syncthreads();
     const uint32_t b = (uint32_t)tid / RG::TPB;
     for (int64_t s = s_first; s < p.n; ++s) {
@@ -425,7 +594,13 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         op.tid = tid;
         op.lane = lane;
         op.par = 0;
-        op.begin(b, p.off[((s * RG::NBK) + b) * p.G + w], (uint32_t)tid % RG::TPB == 0);  // this workgroup's segment of list (s, b)
+        const int64_t li = ((s * RG::NBK) + b) * p.G + w;  // (s, b, w)
+        op.lim = s_lim;
+        op.ovf = p.ovf ? p.ovf + (int64_t)w * p.ovf_cap : nullptr;
+        op.ovf_n = &s_ovf_n;
+        op.ovf_cap = p.ovf_cap;
+        op.sbase = (unsigned long long)s << (2 * K);
+        op.begin(b, p.off[li], p.capv ? p.capv[li] : ~0u, (uint32_t)tid % RG::TPB == 0);  // this workgroup's segment of list (s, b)
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
         const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
@@ -433,9 +608,25 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
         stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
-        op.finish();
+        op.finish(p.cnt + li);
         __syncthreads();
     }
+    if (p.ovf != nullptr && tid == 0) {
+        p.ovf_cnt[w] = s_ovf_n;
+        if (s_ovf_n > p.ovf_cap) __hip_atomic_store(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Sampled mode, after R4: the overflow lists' entries added into stage (device-scope
+// atomics; skewed input only).  Nothing when the exact rerun ran.
+__global__ __launch_bounds__(256) void radix_overflow_kernel(RParams p) {
+    if (__hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+    const int64_t w = blockIdx.x;
+    const uint32_t c = p.ovf_cnt[w];
+    const uint32_t n = c < p.ovf_cap ? c : p.ovf_cap;
+    const unsigned long long *o = p.ovf + w * (int64_t)p.ovf_cap;
+    for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < n; i += gridDim.y * 256)
+        atomicAdd(&p.stage[o[i]], 1u);
 }
 
 // R4: one workgroup per list (s, b).
@@ -494,17 +685,81 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
     }
 }
 
-// Cold path of R4 (LOW = 16): the list recounted exactly in two 32 768-bin
-// halves with 32-bit bins (kept out of line: the hot loop's registers).
+// Sampled mode: a list is the G regions [rb[r], rb[r] + rn[r]) of its workgroups,
+// with gaps between them.  The regions' 16-byte vectors are numbered 0 .. V-1 in
+// order (vpre: exclusive prefix of each region's vector count) and thread t takes
+// vectors t, t + 1024, ..., KMC_R4_U in flight, walking its region cursor forward;
+// a vector's entries outside its region are skipped.
+constexpr int kMaxRegions = 256;  // workgroups of R1/R3 in sampled mode
 template <int LOW>
-__device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uint64_t end, uint32_t *h,
+__device__ __forceinline__ void hist_regions(const uint16_t *ent, const uint32_t *vpre, const unsigned long long *rb,
+                                             const uint32_t *rn, uint32_t *h) {
+    const uint32_t V = vpre[kMaxRegions];
+    const uint4 *v = reinterpret_cast<const uint4 *>(ent);
+    // the thread's current region r, cached in registers: flat vectors [vb, ve),
+    // address of vector vb, and [jf, jl) the ones whose 8 entries all lie in it
+    uint32_t r = 0, vb = 0, ve = 0, jf = 0, jl = 0;
+    unsigned long long va0 = 0;
+    const auto enter = [&](uint32_t q) {
+        vb = vpre[q];
+        ve = vpre[q + 1];
+        const unsigned long long lo = rb[q], hi = lo + rn[q];
+        va0 = lo >> 3;
+        jf = vb + ((lo & 7u) ? 1u : 0u);
+        jl = ve - (((hi & 7u) && ve > jf) ? 1u : 0u);
+    };
+    enter(0);
+    for (uint32_t j0 = threadIdx.x; j0 < V; j0 += KMC_R4_U * 1024) {
+        uint4 x[KMC_R4_U];
+        uint32_t m[KMC_R4_U];  // valid entries of vector u (bit q: entry q)
+#pragma unroll
+        for (int u = 0; u < KMC_R4_U; ++u) {
+            const uint32_t j = j0 + 1024u * u;
+            m[u] = 0u;
+            if (j < V) {
+                while (j >= ve) enter(++r);
+                const unsigned long long va = va0 + (j - vb);
+                x[u] = v[va];
+                if (j >= jf && j < jl) {
+                    m[u] = 0xFFu;
+                } else {  // a region's first or last vector: entries [lo, lo + rn) of it
+                    const int64_t dlo = (int64_t)(rb[r] - va * 8), dhi = dlo + (int64_t)rn[r];
+                    const uint32_t mlo = dlo <= 0 ? 0xFFu : ((0xFFu << dlo) & 0xFFu);
+                    const uint32_t mhi = dhi >= 8 ? 0xFFu : (dhi <= 0 ? 0u : ((1u << dhi) - 1u));
+                    m[u] = mlo & mhi;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < KMC_R4_U; ++u) {
+            const uint32_t e[8] = {x[u].x & 0xFFFFu, x[u].x >> 16, x[u].y & 0xFFFFu, x[u].y >> 16,
+                                   x[u].z & 0xFFFFu, x[u].z >> 16, x[u].w & 0xFFFFu, x[u].w >> 16};
+            if (m[u] == 0xFFu) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) hist_add<LOW>(h, e[q]);
+            } else if (m[u] != 0u) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if ((m[u] >> q) & 1u) hist_add<LOW>(h, e[q]);
+            }
+        }
+    }
+}
+
+// Cold path of R4 (LOW = 16): the list recounted exactly in two 32 768-bin
+// halves with 32-bit bins (kept out of line: the hot loop's registers); the list
+// is [beg, end), or (nreg > 0, sampled mode) the LDS regions [rb[r], rb[r] + rn[r]).
+template <int LOW>
+__device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uint64_t end,
+                                          const unsigned long long *rb, const uint32_t *rn, int nreg, uint32_t *h,
                                           uint32_t *dst) {
     constexpr int kWords = 1 << (LOW - 1);
     for (uint32_t half = 0; half < 2; ++half) {
         __syncthreads();
         for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         __syncthreads();
-        hist_list<LOW, true>(ent, beg, end, h, half);
+        if (nreg == 0) hist_list<LOW, true>(ent, beg, end, h, half);
+        for (int r = 0; r < nreg; ++r) hist_list<LOW, true>(ent, rb[r], rb[r] + rn[r], h, half);
         __syncthreads();
         for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
     }
@@ -515,20 +770,69 @@ __device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uin
 // list wraps, which lowers the sum of the bins below the list length (a carry
 // into the neighbour costs 65 535, one out of the word 65 536), and the list is
 // then recounted exactly in two 32 768-bin halves.
-template <int LOW>
+// REG (sampled mode): the list is the regions (off, min(cnt, capacity)) of the
+// workgroups whose home ranges hold windows of record s (all of cnt when the exact
+// rerun ran: then the regions are contiguous).
+template <int K, bool REG>
 __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbins) {
+    constexpr int LOW = low_bits(K);
     constexpr int kBucketBins = 1 << LOW;
     constexpr int kWords = LOW <= 15 ? kBucketBins : kBucketBins / 2;
     __shared__ __attribute__((aligned(16))) uint32_t h[kWords];
     __shared__ unsigned long long s_sum;
+    __shared__ uint32_t s_vpre[REG ? kMaxRegions + 1 : 1];
+    __shared__ unsigned long long s_rb[REG ? kMaxRegions : 1];
+    __shared__ uint32_t s_rn[REG ? kMaxRegions : 1];
+    __shared__ uint64_t s_scan[kScanBlock / 64];
     const int64_t nlists = p.n * p.nbk;
     for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
         const int64_t s = list / p.nbk, b = list % p.nbk;
         for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         if (threadIdx.x == 0) s_sum = 0ull;
-        __syncthreads();
-        const uint64_t beg = p.off[list * p.G], end = p.off[(list + 1) * p.G];
-        hist_list<LOW, false>(p.ent, beg, end, h, 0u);
+        uint64_t beg, end;  // entries of the list (REG: beg = 0, end = their number)
+        int nreg = 0;
+        if constexpr (REG) {
+            const int t = threadIdx.x;
+            // the home ranges [wf, wf + nreg) that hold windows of record s
+            const Geom g = make_geom<int64_t>(p);
+            int64_t ca, ce;
+            record_windows<K, int64_t>(p, g, s, ca, ce);
+            int64_t wf = 0;
+            if (ce > ca) {
+                wf = ((ca >> kTileShift) - g.T0) / g.tpw;
+                const int64_t wl = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
+                nreg = (int)(wl - wf + 1);
+            }
+            const bool rerun = __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+            uint64_t nv = 0, ne = 0;
+            if (t < nreg) {
+                const int64_t li = list * p.G + wf + t;
+                const unsigned long long rb = p.off[li];
+                ne = p.cnt[li];
+                if (!rerun && ne > p.capv[li]) ne = p.capv[li];  // the rest went to the overflow list
+                nv = ne ? ((rb + ne + 7) >> 3) - (rb >> 3) : 0;
+                s_rb[t] = rb;
+                s_rn[t] = (uint32_t)ne;
+            } else if (t < kMaxRegions) {
+                s_rb[t] = 0;
+                s_rn[t] = 0;
+            }
+            uint64_t tot;
+            const uint64_t ex = block_excl_scan(nv, s_scan, tot);
+            if (t <= kMaxRegions) s_vpre[t] = (uint32_t)ex;
+            beg = 0;
+            end = 0;
+            __syncthreads();
+            uint64_t etot;
+            block_excl_scan(ne, s_scan, etot);
+            end = etot;
+            hist_regions<LOW>(p.ent, s_vpre, s_rb, s_rn, h);
+        } else {
+            __syncthreads();
+            beg = p.off[list * p.G];
+            end = p.off[(list + 1) * p.G];
+            hist_list<LOW, false>(p.ent, beg, end, h, 0u);
+        }
         __syncthreads();
         uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
         if constexpr (LOW <= 15) {
@@ -544,7 +848,7 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
                     reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
                 }
             } else {  // a bin wrapped: exact recount, half of the bins at a time
-                hist_recount<LOW>(p.ent, beg, end, h, dst);
+                hist_recount<LOW>(p.ent, beg, end, s_rb, s_rn, REG ? nreg : 0, h, dst);
             }
         }
         __syncthreads();  // h and s_sum are reused by the next list
@@ -639,11 +943,11 @@ __global__ __launch_bounds__(256) void radix_invalid_kernel(RParams p) {
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct RLayout {
-    size_t cnt, off, bsum, ent, stage, total;
+    size_t cnt, off, bsum, capv, flag, ovf_cnt, ovf, ent, stage, total;
     int64_t m, nscan;
 };
 
-inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap) {
+inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap, bool sampled, uint32_t ovf_cap) {
     RLayout L;
     const int64_t nbk = (int64_t)1 << (2 * k - low_bits(k));
     L.m = n * nbk * G;
@@ -655,6 +959,14 @@ inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap) {
     o += al256((size_t)(L.m + 1) * 8);
     L.bsum = o;
     o += al256((size_t)(L.nscan + 1) * 8);
+    L.capv = o;
+    o += sampled ? al256((size_t)L.m * 4) : 0;
+    L.flag = o;
+    o += sampled ? 256 : 0;
+    L.ovf_cnt = o;
+    o += sampled ? al256((size_t)G * 4) : 0;
+    L.ovf = o;
+    o += sampled ? al256((size_t)G * ovf_cap * 8) : 0;
     L.ent = o;
     o += al256((size_t)ent_cap * 2 + 16);
     L.stage = o;
@@ -665,6 +977,17 @@ inline RLayout r_layout(int k, int64_t n, int G, int64_t ent_cap) {
 
 std::mutex r_mu;
 std::vector<int> r_cus;  // CUs per device
+
+// Partition offsets (kmc_diag_radix_mode): 0 = auto, 1 = exact (R1 count + scan),
+// 2 = sampled (regions sized from a 1-in-8 tile sample, exact rerun on overflow);
+// cap_scale multiplies the sampled capacities (test hook: < 1 forces the rerun).
+int g_radix_mode = 0;
+float g_cap_scale = 1.0f;
+
+// Sampled mode pays when the (record, bucket, workgroup) regions are large: it
+// replaces R1's full read of the input by a 1-in-8 sample plus a capacity margin
+// per region, and R4 then walks G regions per list.
+constexpr double kSampledMinPerRegion = 4096.0;
 
 int r_grid(int device, int &G) {
     std::lock_guard<std::mutex> lk(r_mu);
@@ -697,8 +1020,25 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
     const int64_t tiles = wh > wl ? ((wh + kTile - 1) >> kTileShift) - (wl >> kTileShift) : 0;
     if (tiles < G) G = tiles > 0 ? (int)tiles : 1;
     const int64_t n = (int64_t)a->num_seqs;
-    const int64_t ent_cap = wh > wl ? wh - wl : 0;  // >= valid windows in range
-    const RLayout L = r_layout(K, n, G, ent_cap);
+    constexpr int64_t NBK = (int64_t)1 << (2 * K - low_bits(K));
+    const double win = wh > wl ? (double)(wh - wl) : 0.0;       // >= valid windows in range
+    const double regions = (double)(G + n) * (double)NBK;       // >= (s, b, w) with a piece
+    int mode;
+    float cap_scale;
+    {
+        std::lock_guard<std::mutex> lk(r_mu);
+        mode = g_radix_mode;
+        cap_scale = g_cap_scale;
+    }
+    const bool sampled = G <= kMaxRegions &&
+                         (mode == 2 || (mode == 0 && win >= kSampledMinPerRegion * regions));
+    // sampled capacities: sum over regions of 1.05 c + 6 sqrt(8 c) + 64 (+ 31 rounding),
+    // c summing to the windows; Cauchy-Schwarz bounds the square roots
+    const int64_t ent_cap = sampled ? (int64_t)(1.05 * win + 95.0 * regions + 6.0 * std::sqrt(8.0 * win * regions) + 64.0)
+                                    : (int64_t)win;
+    // overflow lists: 1/32 of the windows in all (past that, the exact rerun)
+    const uint32_t ovf_cap = (uint32_t)std::min<double>(std::max<double>(4096.0, win / 32.0 / G), 1 << 30);
+    const RLayout L = r_layout(K, n, G, ent_cap, sampled, ovf_cap);
     if (size_only) {
         *size_out = L.total;
         return 0;
@@ -742,20 +1082,56 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
     p.sum = a->sum;
     p.ld = a->sum_ld ? (int64_t)a->sum_ld : n;
     p.invalid = a->invalid;
+    p.capv = nullptr;
+    p.flag = nullptr;
+    p.gate = nullptr;
+    p.ovf = nullptr;
+    p.ovf_cnt = nullptr;
+    p.ovf_cap = 0;
+    p.ent_cap = (uint64_t)ent_cap;
+    p.cap_scale = cap_scale;
     uint64_t *bsum = reinterpret_cast<uint64_t *>(base + L.bsum);
     const int64_t nbins = (int64_t)1 << (2 * K);
+    const unsigned hist_grid = (unsigned)std::min<int64_t>(n * p.nbk, kMaxGridX);
 
     if (t_trace_before) {
         he = hipEventRecord(t_trace_before, st);
         if (he != hipSuccess) return (int)he;
     }
-    he = hipMemsetAsync(p.cnt, 0, (size_t)L.m * 4, st);
-    if (he != hipSuccess) return (int)he;
-    hipLaunchKernelGGL((radix_count_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
-    excl_scan_u32(p.cnt, L.m, bsum, p.off, st);
-    hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
-    hipLaunchKernelGGL((radix_hist_kernel<low_bits(K)>), dim3((unsigned)std::min<int64_t>(n * p.nbk, kMaxGridX)),
-                       dim3(1024), 0, st, p, nbins);
+    if (sampled) {
+        // S1 sample -> capacities -> region starts -> R3 into the regions; if one
+        // overflowed (or they exceed ent_cap) the gated exact path reruns R1 + scan +
+        // R3 on the device (no host sync); R4 reads (off, cnt) regions either way
+        RParams ps = p;
+        ps.capv = reinterpret_cast<uint32_t *>(base + L.capv);
+        ps.flag = reinterpret_cast<uint32_t *>(base + L.flag);
+        ps.ovf = reinterpret_cast<unsigned long long *>(base + L.ovf);
+        ps.ovf_cnt = reinterpret_cast<uint32_t *>(base + L.ovf_cnt);
+        ps.ovf_cap = ovf_cap;
+        he = hipMemsetAsync(ps.flag, 0, sizeof(uint32_t), st);
+        if (he == hipSuccess) he = hipMemsetAsync(ps.ovf_cnt, 0, (size_t)G * 4, st);
+        if (he != hipSuccess) return (int)he;
+        hipLaunchKernelGGL((radix_count_kernel<K, int64_t, true>), dim3(G), dim3(1024), 0, st, ps);
+        const int64_t cap_blocks = std::min<int64_t>((L.m + 255) / 256, 4096);
+        hipLaunchKernelGGL((radix_cap_kernel<K, int64_t>), dim3((unsigned)(cap_blocks > 0 ? cap_blocks : 1)), dim3(256),
+                           0, st, ps);
+        excl_scan_u32(ps.capv, L.m, bsum, p.off, st);
+        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, ps);
+        RParams px = p;  // (no capacities, no overflow lists)
+        px.gate = ps.flag;
+        hipLaunchKernelGGL((radix_count_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, px);
+        excl_scan_u32(p.cnt, L.m, bsum, p.off, st, ps.flag);
+        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, px);
+        hipLaunchKernelGGL((radix_hist_kernel<K, true>), dim3(hist_grid), dim3(1024), 0, st, ps, nbins);
+        hipLaunchKernelGGL(radix_overflow_kernel, dim3((unsigned)G, 16), dim3(256), 0, st, ps);
+    } else {
+        he = hipMemsetAsync(p.cnt, 0, (size_t)L.m * 4, st);
+        if (he != hipSuccess) return (int)he;
+        hipLaunchKernelGGL((radix_count_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
+        excl_scan_u32(p.cnt, L.m, bsum, p.off, st);
+        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
+        hipLaunchKernelGGL((radix_hist_kernel<K, false>), dim3(hist_grid), dim3(1024), 0, st, p, nbins);
+    }
     if (p.ld == n && n > kPlaceS && n <= kPlaceMaxN) {  // n <= 16: one tile row covers every record
         const int64_t blocks = (nbins * n + kPlaceO - 1) / kPlaceO;
         hipLaunchKernelGGL(radix_place_contig_kernel, dim3((unsigned)std::min<int64_t>(blocks, kMaxGridX)), dim3(256),
@@ -778,6 +1154,15 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
 }
 
 }  // namespace
+
+// Test hook (not in kmc.h): see g_radix_mode.
+extern "C" int kmc_diag_radix_mode(int mode, float cap_scale) {
+    if (mode < 0 || mode > 2 || !(cap_scale > 0.0f)) return KMC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(r_mu);
+    g_radix_mode = mode;
+    g_cap_scale = cap_scale;
+    return KMC_OK;
+}
 
 // Entry used by kmc_dense.hip for 9 <= k <= KMC_DENSE_MAX_K.
 int radix_dense(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_only, size_t *size_out) {

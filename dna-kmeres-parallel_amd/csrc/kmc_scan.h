@@ -39,8 +39,15 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, ui
     return before + x - v;
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t *in, int64_t m, uint64_t *bsum) {
+// gate (optional): the launch does nothing unless *gate != 0 (a conditional rerun)
+__device__ __forceinline__ bool scan_gated_off(const uint32_t *gate) {
+    return gate != nullptr && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t *in, int64_t m, uint64_t *bsum,
+                                                                 const uint32_t *gate) {
     __shared__ uint64_t sh[kScanBlock / 64];
+    if (scan_gated_off(gate)) return;
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
     uint64_t v = 0;
     for (int q = 0; q < kScanPer; ++q) {
@@ -52,8 +59,9 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint32_t 
     if (threadIdx.x == 0) bsum[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_blocks_kernel(uint64_t *bsum, int64_t nb) {
+__global__ __launch_bounds__(kScanBlock) void scan_blocks_kernel(uint64_t *bsum, int64_t nb, const uint32_t *gate) {
     __shared__ uint64_t sh[kScanBlock / 64];
+    if (scan_gated_off(gate)) return;
     uint64_t carry = 0;
     for (int64_t base = 0; base < nb; base += kScanBlock) {
         const int64_t i = base + threadIdx.x;
@@ -66,8 +74,9 @@ __global__ __launch_bounds__(kScanBlock) void scan_blocks_kernel(uint64_t *bsum,
 }
 
 __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t *in, int64_t m, const uint64_t *bsum,
-                                                                uint64_t *out) {
+                                                                uint64_t *out, const uint32_t *gate) {
     __shared__ uint64_t sh[kScanBlock / 64];
+    if (scan_gated_off(gate)) return;
     const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
     uint64_t v[kScanPer], tsum = 0;
     for (int q = 0; q < kScanPer; ++q) {
@@ -83,14 +92,16 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t *
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanBlock - 1) out[m] = run;  // grand total
 }
 
-// out[0..m] = exclusive scan of in[0..m) (out[m] = total); bsum: scan_tiles(m) uint64
+// out[0..m] = exclusive scan of in[0..m) (out[m] = total); bsum: scan_tiles(m) uint64;
+// gate: see scan_gated_off
 inline int64_t scan_tiles(int64_t m) { return (m + kScanTile - 1) / kScanTile; }
 
-inline void excl_scan_u32(const uint32_t *in, int64_t m, uint64_t *bsum, uint64_t *out, hipStream_t st) {
+inline void excl_scan_u32(const uint32_t *in, int64_t m, uint64_t *bsum, uint64_t *out, hipStream_t st,
+                          const uint32_t *gate = nullptr) {
     const int64_t nt = scan_tiles(m) > 0 ? scan_tiles(m) : 1;
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nt), dim3(kScanBlock), 0, st, in, m, bsum);
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kScanBlock), 0, st, bsum, nt);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nt), dim3(kScanBlock), 0, st, in, m, bsum, out);
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nt), dim3(kScanBlock), 0, st, in, m, bsum, gate);
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kScanBlock), 0, st, bsum, nt, gate);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nt), dim3(kScanBlock), 0, st, in, m, bsum, out, gate);
 }
 
 }  // namespace

@@ -72,6 +72,7 @@ def lib():
         L.kmc_count_dense_ex_workspace_size.restype = ctypes.c_size_t
         L.kmc_count_dense_ex_workspace_size.argtypes = [ctypes.POINTER(DenseArgs), ctypes.c_int]
         L.kmc_trace_set_events.argtypes = [_P, _P]
+        L.kmc_set_reserved_cus.argtypes = [ctypes.c_int]
         L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
         L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.kmc_multi_release.argtypes = []
@@ -97,6 +98,8 @@ def lib():
         L.kmc_pair_distances_workspace_size.argtypes = [_U64, ctypes.c_int, ctypes.c_int]
         L.kmc_pair_distances.argtypes = [_P, _U64, _P, _U64, ctypes.c_int, _P, _P, ctypes.c_size_t, _P]
         L.minKmeres2_hip.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P, _P]
+        if hasattr(L, "kmc_diag_radix_mode"):  # test hook (not in kmc.h; absent from older builds)
+            L.kmc_diag_radix_mode.argtypes = [ctypes.c_int, ctypes.c_float]
         L.kmc_count_canonical_hash.argtypes = [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _P, _P, _U64, _P,
                                                ctypes.POINTER(_U64), _P]
         _lib = L
@@ -255,6 +258,11 @@ def trace_events(before=None, after=None):
     b = ctypes.c_void_p(before._as_parameter_.value) if before is not None else None
     a = ctypes.c_void_p(after._as_parameter_.value) if after is not None else None
     _check(lib().kmc_trace_set_events(b, a), "kmc_trace_set_events")
+
+
+def set_reserved_cus(n):
+    """Leave n CUs out of the dense (k <= 8) grid, for a concurrent kernel (kmc.h)."""
+    _check(lib().kmc_set_reserved_cus(int(n)), "kmc_set_reserved_cus")
 
 
 def synth_fill(data, num_records, record_len, seed, first_base=0, stream=None):

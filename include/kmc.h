@@ -226,6 +226,16 @@ typedef struct ihipEvent_t *hipEvent_t; /* identical to HIP's own typedef */
 int kmc_trace_set_events(hipEvent_t before, hipEvent_t after);
 
 /* ------------------------------------------------------------------------ */
+/* Launch shaping for overlapped collectives (no reference counterpart): the k <= 8
+ * dense kernel runs one 1024-thread workgroup per CU over static byte ranges, so a
+ * CU that another kernel holds when a count starts (an RCCL all-reduce overlapping
+ * the next step, bench.py at N > 1) delays the whole launch.  With n > 0 the
+ * following dense calls of the process launch n workgroups fewer, leaving n CUs to
+ * the concurrent kernel (0 <= n <= 64; 0 = every CU, the default).  The workspace
+ * size depends on it: query kmc_count_dense_ex_workspace_size after setting it. */
+int kmc_set_reserved_cus(int n);
+
+/* ------------------------------------------------------------------------ */
 /* Synthetic input generator (benchmark layout): num_records
  * records of record_len bases, each followed by one '\0'; base g (global index
  * first_base + r*record_len + i) is "ACGT"[(x_{g/32} >> 2*(g%32)) & 3] where x_n

@@ -7,8 +7,9 @@ and, once it is done, a spin kernel (scripts/spin_kernel.hip: `nwg` workgroups
 holding 64 KB of LDS each, so a 128 KB count workgroup cannot share their CU) for
 `us` microseconds on a second stream, exactly as an all-reduce of that step's
 matrix would start while the next step counts.  Prints the per-step time and the
-histogram kernel's time (HIP events) with and without the spin.
-Usage: python scripts/interfere.py [--worlds 1,8] [--nwgs 0,4,8,16,32] [--us 50]"""
+histogram kernel's time (HIP events) with and without the spin, and with the dense
+grid leaving `reserve` CUs free (kmc_set_reserved_cus).
+Usage: python scripts/interfere.py [--worlds 1,8] [--nwgs 0,4,8,16,32] [--us 50] [--reserve 0,8]"""
 import argparse
 import ctypes
 import json
@@ -27,6 +28,7 @@ def main():
     ap.add_argument("--us", type=float, default=50.0)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--reserve", default="0")
     a = ap.parse_args()
     import torch
 
@@ -49,14 +51,18 @@ def main():
         kmc.synth_fill_range(data, base, hold_hi, L, seed)
         idx = torch.from_numpy(plan["indices"]).to(dev)
         out = torch.empty((nb, plan["n_tot"]), dtype=torch.int32, device=dev)
-        args = kmc.dense_args(data, idx, k, out.view(-1), read=(rl, rh), win=(wl, wh), data_offset=base)
-        ws = torch.empty(max(kmc.dense_ex_workspace_size(args), 1), dtype=torch.uint8, device=dev)
-        args = kmc.dense_args(data, idx, k, out.view(-1), read=(rl, rh), win=(wl, wh), workspace=ws, data_offset=base)
-        for _ in range(16):
-            kmc.count_dense_ex(args, s1)
-        torch.cuda.synchronize()
-        ref = out.clone()
-        for rep in range(2):  # two passes over the modes: the box's clock drift shows
+        ref = None
+        for rep, reserve in [(r, v) for r in range(2) for v in [int(x) for x in a.reserve.split(",")]]:
+            # (two passes over the modes: the box's clock drift shows)
+            kmc.set_reserved_cus(reserve)
+            args = kmc.dense_args(data, idx, k, out.view(-1), read=(rl, rh), win=(wl, wh), data_offset=base)
+            ws = torch.empty(max(kmc.dense_ex_workspace_size(args), 1), dtype=torch.uint8, device=dev)
+            args = kmc.dense_args(data, idx, k, out.view(-1), read=(rl, rh), win=(wl, wh), workspace=ws, data_offset=base)
+            for _ in range(16):
+                kmc.count_dense_ex(args, s1)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = out.clone()
             for nwg in [int(x) for x in a.nwgs.split(",")]:
                 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                       for _ in range(a.steps)]
@@ -80,10 +86,13 @@ def main():
                 kmc.trace_events(None, None)
                 kern = sorted(b.elapsed_time(e) for b, e in ev)
                 ok = bool(torch.equal(out, ref))
-                print(json.dumps({"world": world, "pass": rep, "spin_wgs": nwg, "spin_us": a.us if nwg else 0,
+                print(json.dumps({"world": world, "pass": rep, "reserve": reserve, "spin_wgs": nwg,
+                                  "spin_us": a.us if nwg else 0,
                                   "step_ms": round(dt, 4), "kernel_ms_med": round(kern[len(kern) // 2], 4),
                                   "kernel_ms_max": round(kern[-1], 4), "counts_unchanged": ok}), flush=True)
-        del data, out, ws
+            del ws
+        kmc.set_reserved_cus(0)
+        del data, out
         torch.cuda.empty_cache()
 
 

@@ -203,6 +203,72 @@ def test_radix_wrapping_bins_recounted(kmc, oracle, cuda, k):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
+@pytest.fixture
+def radix_mode(kmc):
+    """kmc_diag_radix_mode(mode, cap_scale): 0 auto, 1 exact offsets, 2 sampled
+    regions; cap_scale < 1 shrinks the sampled capacities so regions overflow and
+    the gated exact rerun takes over.  Restored to auto afterwards."""
+    hook = kmc.lib().kmc_diag_radix_mode
+    yield hook
+    assert hook(0, 1.0) == 0
+
+
+@pytest.mark.parametrize("k", [9, 10, 11, 12, 13])
+@pytest.mark.parametrize("scale", [1.0, 0.97, 0.25])
+def test_radix_sampled_regions_vs_oracle(kmc, oracle, cuda, radix_mode, k, scale):
+    """The sampled partition (C3's path): R1 replaced by a 1-in-8 tile sample that
+    sizes a region per (record, bucket, workgroup), R3 writing into the regions and
+    R4 walking them.  scale 1: regions fit; 0.97: a few overflow, 0.25: most do --
+    either way the device-side exact rerun must give the oracle's counts.  Random
+    records (short ones, tile edges, multi-MB) and the skewed poly-A / poly-AC mix
+    (ring overflows, R4 bin wraps)."""
+    assert radix_mode(2, scale) == 0
+    rng = np.random.default_rng(7000 + k)
+    data, idx = random_records(rng, [0, 1, k, 1025, 300_000, 17, 2_000_003, 4_500_000], 0.003, 0.003, 0.001)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    mixed = np.concatenate([acgt[rng.integers(0, 4, 500_000)], np.full(300_000, ord("A"), np.uint8),
+                            acgt[rng.integers(0, 4, 200_000)], np.frombuffer(b"AC" * 70_000, np.uint8)])
+    recs = [np.append(mixed, np.uint8(0)), np.append(acgt[rng.integers(0, 4, 3_000_000)], np.uint8(0))]
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
+@pytest.mark.parametrize("scale", [1.0, 0.5])
+def test_radix_sampled_shards_and_workspace(kmc, oracle, cuda, radix_mode, scale):
+    """Sampled partition over byte-range shards (window range + halo) with a caller
+    workspace sized by kmc_count_dense_ex_workspace_size: the shards sum to the
+    whole histogram."""
+    import torch
+    assert radix_mode(2, scale) == 0
+    k = 13
+    rng = np.random.default_rng(91)
+    data, idx = random_records(rng, [2_600_000, 5, 1_400_001], 0.002, 0.002)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    acc = np.zeros_like(exp)
+    inv_acc = np.zeros_like(exp_inv)
+    for a, b, rl, rh in kmc.plan_shards(idx, k, 3):
+        out = torch.full((1 << (2 * k), idx.size - 1), -1, dtype=torch.int32, device=cuda)
+        inv = torch.full((idx.size - 1,), -1, dtype=torch.int32, device=cuda)
+        args = kmc.dense_args(d, di, k, out, read=(rl, rh), win=(a, b), invalid=inv)
+        ws = torch.empty(kmc.dense_ex_workspace_size(args), dtype=torch.uint8, device=cuda)
+        kmc.count_dense_ex(kmc.dense_args(d, di, k, out, read=(rl, rh), win=(a, b), invalid=inv, workspace=ws))
+        torch.cuda.synchronize()
+        acc += out.cpu().numpy()
+        inv_acc += inv.cpu().numpy()
+        del out, ws
+    np.testing.assert_array_equal(acc, exp)
+    np.testing.assert_array_equal(inv_acc, exp_inv)
+
+
 @pytest.mark.parametrize("k", [11, 13])
 def test_radix_shards_sum_to_full(kmc, oracle, cuda, k):
     import torch
