@@ -64,6 +64,9 @@ def parse(argv=None):
                     help="HBM traffic per launch measured by rocprofv3 --pmc, per shard size (see profiles/)")
     ap.add_argument("--allreduce-reps", type=int, default=20,
                     help="N > 1: all-reduces timed alone after the timed region")
+    ap.add_argument("--reserve-cus", type=int, default=-1,
+                    help="CUs left out of the histogram grid for the overlapped all-reduce, whose RCCL "
+                         "channels are capped to match (NCCL_MAX_NCHANNELS); -1 = 8 at N > 1, 0 at N = 1")
     return ap.parse_args(argv)
 
 
@@ -279,6 +282,16 @@ def main():
     # one GPU of a test box (RCCL needs one device per rank); never a measurement
     backend = os.environ.get("KMC_BENCH_BACKEND", "nccl")
     local = local % torch.cuda.device_count() if backend != "nccl" else local
+    # each step's all-reduce overlaps the next step's counting; the histogram grid is
+    # one static workgroup per CU, so a CU held by RCCL delays the launch (+12 % per
+    # step at 8-way with 8 CUs held for 50 us, scripts/interfere.py).  Leaving
+    # reserve_cus CUs to RCCL, its channels capped to as many, keeps them apart
+    # (the same experiment: 0.348-0.351 -> 0.318 ms; 0.311 -> 0.318 ms alone).
+    reserve = args.reserve_cus if args.reserve_cus >= 0 else (8 if world > 1 else 0)
+    if world > 1 and reserve > 0:
+        os.environ.setdefault("NCCL_MAX_NCHANNELS", str(reserve))
+    kmc.set_reserved_cus(reserve)
+    args.reserve_cus_eff = reserve
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -478,6 +491,8 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
                            "split over the GPUs" if args.scaling == "strong" else "%d records per GPU" % args.records),
             "k": k, "total_records": n_tot, "record_len": L, "bins": nb, "parallelism": par,
             "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "reserved_cus": getattr(args, "reserve_cus_eff", None),
+            "rccl_max_channels": os.environ.get("NCCL_MAX_NCHANNELS") if world > 1 else None,
             "backend": dist.get_backend() if world > 1 else "none (1 GPU)",
         },
         "roofline": {

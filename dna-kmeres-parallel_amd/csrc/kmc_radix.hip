@@ -326,7 +326,9 @@ __device__ __forceinline__ uint32_t ring_word(uint32_t b, uint32_t f0) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
-template <int K>
+// SAMPLED: regions with capacities and overflow lists (radix_count_kernel<SAMPLE>);
+// otherwise exact offsets, and none of that code.
+template <int K, bool SAMPLED>
 struct RRingOp {
     using RG = RingGeom<K>;
     uint16_t *ring;        // LDS, NBK * RING entries
@@ -355,15 +357,15 @@ struct RRingOp {
     __device__ void before_tile() {}
 
     // an entry e of bucket b past its region -> the overflow list (added into stage
-    // by radix_overflow_kernel after R4; a full list raises the exact rerun).  Out of
-    // line, like ovf_seg: cold paths, kept out of the hot loop's code and registers.
-    __device__ __noinline__ void ovf_put(uint32_t b, uint32_t e) const {
+    // by radix_overflow_kernel after R4; a full list raises the exact rerun).  (Out
+    // of line, this and ovf_seg made R3 5 % slower: calls, a stack, spills.)
+    __device__ __forceinline__ void ovf_put(uint32_t b, uint32_t e) const {
         const uint32_t i = atomicAdd(ovf_n, 1u);
         if (i < ovf_cap) ovf[i] = sbase + ((unsigned long long)b << RG::LOW) + e;
     }
     // this lane's 8 entries (x) of a complete segment past its region, whose ring
     // LDS address is a & ~63
-    __device__ __noinline__ void ovf_seg(uint32_t a, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) const {
+    __device__ __forceinline__ void ovf_seg(uint32_t a, uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) const {
         const uint32_t bt = ((a & ~63u) - (uint32_t)(uintptr_t)ring) / (2u * RG::RING);
         const uint32_t i8 = atomicAdd(ovf_n, 8u);
         const uint32_t w4[4] = {x0, x1, x2, x3};
@@ -421,7 +423,7 @@ struct RRingOp {
                     const uint32_t bj = (c[j] >> RG::LOW) & (RG::NBK - 1);
                     const unsigned long long at = gH[bj] + lo;
                     const uint32_t e = c[j] & ((1u << RG::LOW) - 1u);
-                    if (at < lim[bj]) ent[at] = (uint16_t)e;
+                    if (!SAMPLED || at < lim[bj]) ent[at] = (uint16_t)e;
                     else ovf_put(bj, e);
                 }
             }
@@ -439,11 +441,11 @@ struct RRingOp {
     __device__ __forceinline__ void begin(uint32_t b, unsigned long long F, uint32_t capb, bool owner) {
         P0 = F & ~31ull;
         f = v = f0 = (uint32_t)(F - P0);
-        cap = capb == ~0u ? ~0u : f0 + capb;
+        cap = SAMPLED ? f0 + capb : ~0u;
         if (owner) {
             W[b] = ring_word<K>(b, f);
             gH[b] = P0;
-            lim[b] = capb == ~0u ? ~0ull : P0 + cap;
+            if (SAMPLED) lim[b] = P0 + cap;
         }
     }
 
@@ -476,7 +478,7 @@ struct RRingOp {
             for (uint32_t q = 0; q < 32; ++q)
                 if (h + q >= v) {
                     const uint16_t e = ring_entry(b, h, h + q);
-                    if (h + q < cap) ent[P0 + h + q] = e;
+                    if (!SAMPLED || h + q < cap) ent[P0 + h + q] = e;
                     else ovf_put(b, e);
                 }
             i0 = j + RG::TPB;
@@ -487,7 +489,7 @@ struct RRingOp {
         for (uint32_t i = i0; __any(i < nseg); i += RG::TPB) {  // mostly once: two segments are rare
             // bit 2: a segment to store, bit 3: one past its region (to the overflow
             // list); bits 0-1: the chunk swizzle
-            const bool in = h + 32u * i + 32u <= cap;
+            const bool in = !SAMPLED || h + 32u * i + 32u <= cap;
             const uint32_t A = (rowb + 64u * (i ^ (x8 >> 2))) | (x8 & 3u) | (i < nseg ? (in ? 4u : 8u) : 0u);
             uint32_t a[4], g[4];
             quad_bcast4(A, a);
@@ -498,7 +500,7 @@ struct RRingOp {
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (a[t] & 4u) reinterpret_cast<u32x4 *>(ent + 32ull * g[t])[q] = val[t];
-            if (__builtin_expect(__any(((a[0] | a[1] | a[2] | a[3]) & 8u) != 0u), 0)) {
+            if (SAMPLED && __builtin_expect(__any(((a[0] | a[1] | a[2] | a[3]) & 8u) != 0u), 0)) {
                 for (int t = 0; t < 4; ++t)  // this lane's 8 entries of the quad's segment t
                     if (a[t] & 8u) ovf_seg(a[t], val[t][0], val[t][1], val[t][2], val[t][3]);
             }
@@ -536,7 +538,7 @@ struct RRingOp {
         const uint32_t lo = h > v ? h : v;
         for (uint32_t g = lo + j; g < f; g += RG::TPB) {
             const uint16_t e = ring_entry(b, h, g);
-            if (g < cap) ent[P0 + g] = e;
+            if (!SAMPLED || g < cap) ent[P0 + g] = e;
             else ovf_put(b, e);
         }
         if (j == 0) *cnt_out = f - f0;
@@ -544,8 +546,9 @@ struct RRingOp {
 };
 
 // R3 launch: the piece walk of radix_count_kernel with the ring scatter (the whole
-// LDS of a CU: one 1024-thread workgroup per CU).
-template <int K, class Idx>
+// LDS of a CU: one 1024-thread workgroup per CU).  SAMPLED: into the capacity
+// regions (p.capv), entries past them to the overflow lists (p.ovf).
+template <int K, class Idx, bool SAMPLED>
 __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
     using RG = RingGeom<K>;
     constexpr int NWAVES = RG::BLOCK / 64;
@@ -560,7 +563,7 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     if (gated_off(p)) return;
     // sampled mode: the capacities must fit the entry array (else the exact rerun)
-    if (p.capv != nullptr && p.off[p.n * RG::NBK * p.G] > p.ent_cap) {
+    if (SAMPLED && p.off[p.n * RG::NBK * p.G] > p.ent_cap) {
         if (tid == 0) __hip_atomic_store(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
@@ -585,7 +588,7 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         const int64_t ps = ca > R0 ? ca : R0;
         const int64_t pe = ce < R1 ? ce : R1;
         if (ps >= pe) continue;
-        RRingOp<K> op;
+        RRingOp<K, SAMPLED> op;
         op.ring = s_ring;
         op.W = s_W;
         op.gH = s_gH;
@@ -600,18 +603,18 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         op.ovf_n = &s_ovf_n;
         op.ovf_cap = p.ovf_cap;
         op.sbase = (unsigned long long)s << (2 * K);
-        op.begin(b, p.off[li], p.capv ? p.capv[li] : ~0u, (uint32_t)tid % RG::TPB == 0);  // this workgroup's segment of list (s, b)
+        op.begin(b, p.off[li], SAMPLED ? p.capv[li] : 0u, (uint32_t)tid % RG::TPB == 0);  // this workgroup's segment of list (s, b)
         __syncthreads();
         const int64_t tp0 = ps >> kTileShift;
         const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
         const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-        stream_tiles<K, RRingOp<K>, KMC_RSCAT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        stream_tiles<K, RRingOp<K, SAMPLED>, KMC_RSCAT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         op.finish(p.cnt + li);
         __syncthreads();
     }
-    if (p.ovf != nullptr && tid == 0) {
+    if (SAMPLED && tid == 0) {
         p.ovf_cnt[w] = s_ovf_n;
         if (s_ovf_n > p.ovf_cap) __hip_atomic_store(p.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -746,19 +749,31 @@ __device__ __forceinline__ void hist_regions(const uint16_t *ent, const uint32_t
     }
 }
 
-// Cold path of R4 (LOW = 16): the list recounted exactly in two 32 768-bin
-// halves with 32-bit bins (kept out of line: the hot loop's registers); the list
-// is [beg, end), or (nreg > 0, sampled mode) the LDS regions [rb[r], rb[r] + rn[r]).
+// Cold path of R4 (LOW = 16): the list [beg, end) recounted exactly in two 32 768-bin
+// halves with 32-bit bins (kept out of line: the hot loop's registers).
 template <int LOW>
-__device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uint64_t end,
-                                          const unsigned long long *rb, const uint32_t *rn, int nreg, uint32_t *h,
+__device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uint64_t end, uint32_t *h,
                                           uint32_t *dst) {
     constexpr int kWords = 1 << (LOW - 1);
     for (uint32_t half = 0; half < 2; ++half) {
         __syncthreads();
         for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         __syncthreads();
-        if (nreg == 0) hist_list<LOW, true>(ent, beg, end, h, half);
+        hist_list<LOW, true>(ent, beg, end, h, half);
+        __syncthreads();
+        for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
+    }
+}
+
+// The same for a list of nreg regions [rb[r], rb[r] + rn[r]) (sampled mode).
+template <int LOW>
+__device__ __noinline__ void hist_recount_regions(const uint16_t *ent, const unsigned long long *rb,
+                                                  const uint32_t *rn, int nreg, uint32_t *h, uint32_t *dst) {
+    constexpr int kWords = 1 << (LOW - 1);
+    for (uint32_t half = 0; half < 2; ++half) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+        __syncthreads();
         for (int r = 0; r < nreg; ++r) hist_list<LOW, true>(ent, rb[r], rb[r] + rn[r], h, half);
         __syncthreads();
         for (int i = threadIdx.x; i < kWords; i += 1024) dst[half * kWords + i] = h[i];
@@ -770,9 +785,8 @@ __device__ __noinline__ void hist_recount(const uint16_t *ent, uint64_t beg, uin
 // list wraps, which lowers the sum of the bins below the list length (a carry
 // into the neighbour costs 65 535, one out of the word 65 536), and the list is
 // then recounted exactly in two 32 768-bin halves.
-// REG (sampled mode): the list is the regions (off, min(cnt, capacity)) of the
-// workgroups whose home ranges hold windows of record s (all of cnt when the exact
-// rerun ran: then the regions are contiguous).
+// REG (sampled mode): the list is the G regions (off, min(cnt, capacity)) of the
+// workgroups (all of cnt when the exact rerun ran: then the regions are contiguous).
 template <int K, bool REG>
 __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbins) {
     constexpr int LOW = low_bits(K);
@@ -785,28 +799,21 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
     __shared__ uint32_t s_rn[REG ? kMaxRegions : 1];
     __shared__ uint64_t s_scan[kScanBlock / 64];
     const int64_t nlists = p.n * p.nbk;
+    // sampled mode: did the exact rerun run (then every region is exact and whole)?
+    const bool rerun = REG && __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
         const int64_t s = list / p.nbk, b = list % p.nbk;
         for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         if (threadIdx.x == 0) s_sum = 0ull;
         uint64_t beg, end;  // entries of the list (REG: beg = 0, end = their number)
-        int nreg = 0;
+        const int nreg = p.G;
         if constexpr (REG) {
+            // every workgroup's region of the list, loaded in one round trip (a
+            // dependent search for the workgroups that hold record s cost more)
             const int t = threadIdx.x;
-            // the home ranges [wf, wf + nreg) that hold windows of record s
-            const Geom g = make_geom<int64_t>(p);
-            int64_t ca, ce;
-            record_windows<K, int64_t>(p, g, s, ca, ce);
-            int64_t wf = 0;
-            if (ce > ca) {
-                wf = ((ca >> kTileShift) - g.T0) / g.tpw;
-                const int64_t wl = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
-                nreg = (int)(wl - wf + 1);
-            }
-            const bool rerun = __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
             uint64_t nv = 0, ne = 0;
             if (t < nreg) {
-                const int64_t li = list * p.G + wf + t;
+                const int64_t li = list * p.G + t;
                 const unsigned long long rb = p.off[li];
                 ne = p.cnt[li];
                 if (!rerun && ne > p.capv[li]) ne = p.capv[li];  // the rest went to the overflow list
@@ -848,7 +855,8 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
                     reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
                 }
             } else {  // a bin wrapped: exact recount, half of the bins at a time
-                hist_recount<LOW>(p.ent, beg, end, s_rb, s_rn, REG ? nreg : 0, h, dst);
+                if constexpr (REG) hist_recount_regions<LOW>(p.ent, s_rb, s_rn, nreg, h, dst);
+                else hist_recount<LOW>(p.ent, beg, end, h, dst);
             }
         }
         __syncthreads();  // h and s_sum are reused by the next list
@@ -984,10 +992,11 @@ std::vector<int> r_cus;  // CUs per device
 int g_radix_mode = 0;
 float g_cap_scale = 1.0f;
 
-// Sampled mode pays when the (record, bucket, workgroup) regions are large: it
-// replaces R1's full read of the input by a 1-in-8 sample plus a capacity margin
-// per region, and R4 then walks G regions per list.
-constexpr double kSampledMinPerRegion = 4096.0;
+// Sampled mode pays when the lists are long: it replaces R1's full read of the
+// input by a 1-in-8 sample (C3: R1 1.95 -> 0.42 ms), but R4 then sets up G regions
+// per list and walks them (C3: +0.1-0.3 ms over 10 240 lists of ~1 M entries; C3R,
+// 25 600 lists of ~120 K entries: +0.6 ms, more than its R1 saving).
+constexpr double kSampledMinPerList = 256.0 * 1024.0;
 
 int r_grid(int device, int &G) {
     std::lock_guard<std::mutex> lk(r_mu);
@@ -1031,7 +1040,7 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
         cap_scale = g_cap_scale;
     }
     const bool sampled = G <= kMaxRegions &&
-                         (mode == 2 || (mode == 0 && win >= kSampledMinPerRegion * regions));
+                         (mode == 2 || (mode == 0 && win >= kSampledMinPerList * (double)n * (double)NBK));
     // sampled capacities: sum over regions of 1.05 c + 6 sqrt(8 c) + 64 (+ 31 rounding),
     // c summing to the windows; Cauchy-Schwarz bounds the square roots
     const int64_t ent_cap = sampled ? (int64_t)(1.05 * win + 95.0 * regions + 6.0 * std::sqrt(8.0 * win * regions) + 64.0)
@@ -1116,12 +1125,12 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
         hipLaunchKernelGGL((radix_cap_kernel<K, int64_t>), dim3((unsigned)(cap_blocks > 0 ? cap_blocks : 1)), dim3(256),
                            0, st, ps);
         excl_scan_u32(ps.capv, L.m, bsum, p.off, st);
-        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, ps);
+        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t, true>), dim3(G), dim3(1024), 0, st, ps);
         RParams px = p;  // (no capacities, no overflow lists)
         px.gate = ps.flag;
         hipLaunchKernelGGL((radix_count_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, px);
         excl_scan_u32(p.cnt, L.m, bsum, p.off, st, ps.flag);
-        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, px);
+        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t, false>), dim3(G), dim3(1024), 0, st, px);
         hipLaunchKernelGGL((radix_hist_kernel<K, true>), dim3(hist_grid), dim3(1024), 0, st, ps, nbins);
         hipLaunchKernelGGL(radix_overflow_kernel, dim3((unsigned)G, 16), dim3(256), 0, st, ps);
     } else {
@@ -1129,7 +1138,7 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
         if (he != hipSuccess) return (int)he;
         hipLaunchKernelGGL((radix_count_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
         excl_scan_u32(p.cnt, L.m, bsum, p.off, st);
-        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t>), dim3(G), dim3(1024), 0, st, p);
+        hipLaunchKernelGGL((radix_ring_kernel<K, int64_t, false>), dim3(G), dim3(1024), 0, st, p);
         hipLaunchKernelGGL((radix_hist_kernel<K, false>), dim3(hist_grid), dim3(1024), 0, st, p, nbins);
     }
     if (p.ld == n && n > kPlaceS && n <= kPlaceMaxN) {  // n <= 16: one tile row covers every record

@@ -72,7 +72,8 @@ def lib():
         L.kmc_count_dense_ex_workspace_size.restype = ctypes.c_size_t
         L.kmc_count_dense_ex_workspace_size.argtypes = [ctypes.POINTER(DenseArgs), ctypes.c_int]
         L.kmc_trace_set_events.argtypes = [_P, _P]
-        L.kmc_set_reserved_cus.argtypes = [ctypes.c_int]
+        if hasattr(L, "kmc_set_reserved_cus"):  # (absent from builds before round 3)
+            L.kmc_set_reserved_cus.argtypes = [ctypes.c_int]
         L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
         L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.kmc_multi_release.argtypes = []
