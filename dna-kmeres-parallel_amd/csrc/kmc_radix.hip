@@ -801,6 +801,19 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
     const int64_t nlists = p.n * p.nbk;
     // sampled mode: did the exact rerun run (then every region is exact and whole)?
     const bool rerun = REG && __hip_atomic_load(p.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    // REG: thread t < G holds region t of the next list, loaded one list ahead so
+    // that the loads' latency hides behind the current list's histogram
+    unsigned long long nx_rb = 0;
+    uint32_t nx_ne = 0;
+    const auto fetch = [&](int64_t L) {
+        if (REG && L < nlists && (int)threadIdx.x < p.G) {
+            const int64_t li = L * p.G + threadIdx.x;
+            nx_rb = p.off[li];
+            const uint32_t c = p.cnt[li], cap = rerun ? c : p.capv[li];
+            nx_ne = c < cap ? c : cap;  // past the capacity: in the overflow list
+        }
+    };
+    fetch(blockIdx.x);
     for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
         const int64_t s = list / p.nbk, b = list % p.nbk;
         for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
@@ -808,31 +821,28 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
         uint64_t beg, end;  // entries of the list (REG: beg = 0, end = their number)
         const int nreg = p.G;
         if constexpr (REG) {
-            // every workgroup's region of the list, loaded in one round trip (a
-            // dependent search for the workgroups that hold record s cost more)
+            // every workgroup's region of the list (a dependent search for the
+            // workgroups that hold record s cost more); one block scan of (vectors,
+            // entries) packed in 64 bits
             const int t = threadIdx.x;
-            uint64_t nv = 0, ne = 0;
+            const unsigned long long rb = nx_rb;
+            const uint32_t ne = nx_ne;
+            fetch(list + gridDim.x);
+            uint64_t nv = 0;
             if (t < nreg) {
-                const int64_t li = list * p.G + t;
-                const unsigned long long rb = p.off[li];
-                ne = p.cnt[li];
-                if (!rerun && ne > p.capv[li]) ne = p.capv[li];  // the rest went to the overflow list
                 nv = ne ? ((rb + ne + 7) >> 3) - (rb >> 3) : 0;
                 s_rb[t] = rb;
-                s_rn[t] = (uint32_t)ne;
+                s_rn[t] = ne;
             } else if (t < kMaxRegions) {
                 s_rb[t] = 0;
                 s_rn[t] = 0;
             }
             uint64_t tot;
-            const uint64_t ex = block_excl_scan(nv, s_scan, tot);
+            const uint64_t ex = block_excl_scan(t < nreg ? nv | ((uint64_t)ne << 32) : 0ull, s_scan, tot);
             if (t <= kMaxRegions) s_vpre[t] = (uint32_t)ex;
             beg = 0;
-            end = 0;
+            end = tot >> 32;
             __syncthreads();
-            uint64_t etot;
-            block_excl_scan(ne, s_scan, etot);
-            end = etot;
             hist_regions<LOW>(p.ent, s_vpre, s_rb, s_rn, h);
         } else {
             __syncthreads();
