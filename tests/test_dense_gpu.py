@@ -402,6 +402,33 @@ def test_range_shards_sum_to_full(kmc, oracle, cuda, k):
     np.testing.assert_array_equal(inv_acc, exp_inv)
 
 
+@pytest.mark.parametrize("k", [3, 8])
+def test_dense_reserved_cus_vs_oracle(kmc, oracle, cuda, k):
+    """kmc_set_reserved_cus (bench.py at N > 1 leaves CUs to the overlapped
+    all-reduce): fewer workgroups, each with a longer home range -- same counts,
+    and a caller workspace sized after the setting."""
+    import torch
+    rng = np.random.default_rng(4400 + k)
+    data, idx = random_records(rng, [3_000_001, 17, 250_000, 1, 4_000_003], 0.002, 0.002, 0.0005)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    try:
+        for reserve in (8, 64):
+            kmc.set_reserved_cus(reserve)
+            out = torch.full((1 << (2 * k), idx.size - 1), -1, dtype=torch.int32, device=cuda)
+            inv = torch.full((idx.size - 1,), -1, dtype=torch.int32, device=cuda)
+            args = kmc.dense_args(d, di, k, out, invalid=inv)
+            ws = torch.empty(kmc.dense_ex_workspace_size(args), dtype=torch.uint8, device=cuda)
+            kmc.count_dense_ex(kmc.dense_args(d, di, k, out, invalid=inv, workspace=ws))
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy(), exp, err_msg="reserve %d" % reserve)
+            np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv, err_msg="reserve %d" % reserve)
+        with pytest.raises(kmc.KmcError):
+            kmc.set_reserved_cus(65)
+    finally:
+        kmc.set_reserved_cus(0)
+
+
 def test_sum_ld_column_block_and_workspace(kmc, oracle, cuda):
     """Writing into columns [off, off+n) of a wider matrix (multi-rank layout),
     with a caller-provided workspace."""
