@@ -8,8 +8,8 @@
 //
 // Hash-partitioned counting, so that no table lives in HBM and no k-mer costs a
 // device-scope atomic.  The input walks partition a window by m = key x C (one
-// multiply, invertible); the lists hold h = fmix64(key) (a bijection; only the
-// distinct keys are unmixed, at output).  Record r has 2^lg_r lists (top lg_r
+// multiply, invertible); the lists hold h = fmix62(key) (a bijection of 62-bit
+// values; only the distinct keys are unmixed, by K5).  Record r has 2^lg_r lists (top lg_r
 // bits of m, about 4 K windows each, lg_r <= 15), grouped in 2^lgc_r coarse
 // buckets (top lgc_r = min(lg_r, 7) bits):
 //   K1 count    workgroups walk contiguous chunk ranges record piece by record
@@ -67,7 +67,7 @@
 namespace kmc {
 namespace {
 
-constexpr uint64_t kEmptyH = 0x64B5720B4B825F21ull;  // fmix64(~0): no k-mer key (< 2^62) hashes to it
+constexpr uint64_t kEmptyH = ~0ull;  // no list value: those are fmix62 outputs, < 2^62
 constexpr int kWalkBlock = 1024;             // K1 / K3a / K3b threads per workgroup
 constexpr int kMaxLg = 15;                   // at most 32 768 lists per record (K1's LDS counters)
 constexpr int kCoarseLg = 7;                 // at most 128 coarse buckets per record
@@ -138,36 +138,41 @@ struct HParams {
     uint32_t *out_counts;
 };
 
-__device__ __forceinline__ uint64_t fmix64(uint64_t h) {  // MurmurHash3 finaliser
-    h ^= h >> 33;
-    h *= 0xFF51AFD7ED558CCDull;
-    h ^= h >> 33;
-    h *= 0xC4CEB9FE1A85EC53ull;
-    h ^= h >> 33;
-    return h;
-}
-
 // Partition value of a key: K1 / K3a / K3b bucket and list by its top bits.  A
-// multiplicative hash (one 64-bit multiply, invertible) instead of fmix64 in
+// multiplicative hash (one 64-bit multiply, invertible) instead of fmix62 in
 // the two input walks; K3b (or K3a for single-list buckets) turns it into
-// fmix64(key) when writing the lists, which is what K4 hashes and unmixes.
+// fmix62(key) when writing the lists, which is what K4 hashes and K5 unmixes.
 constexpr uint64_t kMulC = 0x9E3779B97F4A7C15ull, kMulCinv = 0xF1DE83E19937733Dull;
 __device__ __forceinline__ uint64_t part_of(uint64_t key);
 __device__ __forceinline__ uint64_t list_value(uint64_t m);
 
-__device__ __forceinline__ uint64_t unmix64(uint64_t h) {  // inverse of fmix64
-    h ^= h >> 33;
-    h *= 0x9CB4B2F8129337DBull;
-    h ^= h >> 33;
-    h *= 0x4F74430C22A54005ull;
-    h ^= h >> 33;
+// MurmurHash3's fmix64 rounds on 62-bit values (a k <= 31 key): a bijection of [0, 2^62) --
+// multiplication by an odd constant mod 2^62, and x ^= x >> 31, which is its own
+// inverse on 62 bits -- so a list value leaves the top two bits free, and K4s / K4
+// emit it with the count tag there: the inverse (unmix62, ~20 VALU ops per key)
+// runs in the memory-bound place kernel, not in the issue-bound counting kernels.
+constexpr uint64_t kM62 = (1ull << 62) - 1ull;
+__device__ __forceinline__ uint64_t fmix62(uint64_t h) {
+    h ^= h >> 31;
+    h = (h * 0xFF51AFD7ED558CCDull) & kM62;
+    h ^= h >> 31;
+    h = (h * 0xC4CEB9FE1A85EC53ull) & kM62;
+    h ^= h >> 31;
+    return h;
+}
+__device__ __forceinline__ uint64_t unmix62(uint64_t h) {  // inverse of fmix62
+    h ^= h >> 31;
+    h = (h * 0x9CB4B2F8129337DBull) & kM62;  // (inverses mod 2^64 are inverses mod 2^62)
+    h ^= h >> 31;
+    h = (h * 0x4F74430C22A54005ull) & kM62;
+    h ^= h >> 31;
     return h;
 }
 
 __device__ __forceinline__ uint64_t part_of(uint64_t key) { return key * kMulC; }
 
-__device__ __forceinline__ uint64_t list_value(uint64_t m) {  // partition value -> fmix64(key)
-    return fmix64(m * kMulCinv);
+__device__ __forceinline__ uint64_t list_value(uint64_t m) {  // partition value -> fmix62(key)
+    return fmix62(m * kMulCinv);
 }
 
 // LE 2-bit code (first base in the low bits, the dense path's order) -> MSB-first
@@ -852,7 +857,7 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                     // keys use at most 62 bits (k <= 31): occurrences 1..3 ride in the
                     // top two bits, larger counts escape to pc (K5 reads it only then)
                     const unsigned long long tag = c < 3u ? c : 3u;
-                    p.pk[out + before + i] = unmix64(h) | (tag << 62);
+                    p.pk[out + before + i] = h | (tag << 62);
                     if (c >= 3u) p.pc[out + before + i] = c + 1u;
                 }
             }
@@ -925,7 +930,7 @@ static_assert(2 * KMC_CANON_MAX_K <= 62, "pair format: keys must leave the top t
 __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned long long h, uint32_t cnt) {
     const uint32_t c = cnt - 1u;  // occurrences - 1, as the table kernel stores them
     const unsigned long long tag = c < 3u ? c : 3u;
-    p.pk[o] = unmix64(h) | (tag << 62);
+    p.pk[o] = h | (tag << 62);
     if (c >= 3u) p.pc[o] = cnt;
 }
 
@@ -1133,7 +1138,7 @@ __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
             const uint64_t i = i0 + 256u * u;
             if (i < m) {
                 const uint32_t tag = (uint32_t)(x[u] >> 62);
-                const uint64_t key = x[u] & 0x3FFFFFFFFFFFFFFFull;
+                const uint64_t key = unmix62(x[u] & kM62);
                 const uint32_t cnt = tag < 3u ? tag + 1u : p.pc[src + i];
                 p.out_keys[dst + i] = key;
                 p.out_counts[dst + i] = cnt;
