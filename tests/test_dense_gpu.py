@@ -245,7 +245,7 @@ def test_radix_sampled_regions_vs_oracle(kmc, oracle, cuda, radix_mode, k, scale
 def test_radix_sampled_shards_and_workspace(kmc, oracle, cuda, radix_mode, scale):
     """Sampled partition over byte-range shards (window range + halo) with a caller
     workspace sized by kmc_count_dense_ex_workspace_size: the shards sum to the
-    whole histogram."""
+    whole histogram; and the whole buffer through an unaligned data pointer."""
     import torch
     assert radix_mode(2, scale) == 0
     k = 13
@@ -267,6 +267,13 @@ def test_radix_sampled_shards_and_workspace(kmc, oracle, cuda, radix_mode, scale
         del out, ws
     np.testing.assert_array_equal(acc, exp)
     np.testing.assert_array_equal(inv_acc, exp_inv)
+    # the whole buffer from a data pointer 7 bytes past an aligned one
+    big = torch.zeros(data.size + 48, dtype=torch.uint8, device=cuda)
+    big[7:7 + data.size] = d
+    out, inv = kmc.count_dense(big[7:7 + data.size], di, k, data_bytes=data.size, invalid=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv)
 
 
 @pytest.mark.parametrize("k", [11, 13])
