@@ -2,7 +2,9 @@
 """DIAGNOSTIC fuzz: kmc_count_dense (k = 1..13: LDS kernels, packed 16-bit bins
 with their scans and recounts, the radix path) vs the oracle on random record sets
 with N / lowercase / low-complexity runs; bit-exact counts and invalid counts.
-Usage: python scripts/fuzz_dense.py [--cases 40] [--seed 1]"""
+--sampled: k >= 9 cases take the sampled radix partition, with capacities x 1,
+x 0.9 (overflow lists) or x 0.3 (the exact rerun) at random.
+Usage: python scripts/fuzz_dense.py [--cases 40] [--seed 1] [--sampled]"""
 import argparse
 import os
 import sys
@@ -37,6 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=40)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--sampled", action="store_true")
     a = ap.parse_args()
     import torch
     import kmc
@@ -47,13 +50,20 @@ def main():
     for c in range(a.cases):
         k = int(rng.integers(1, 14))
         data, idx = make_case(rng, k)
+        mode = ""
+        if a.sampled and k >= 9:
+            scale = float(rng.choice([1.0, 0.9, 0.3]))
+            kmc.lib().kmc_diag_radix_mode(2, scale)
+            mode = " sampled x%.1f" % scale
         d = torch.from_numpy(data if data.size else np.zeros(16, np.uint8)).to(dev)
         out, inv = kmc.count_dense(d, torch.from_numpy(idx).to(dev), k, data_bytes=data.size, invalid=True)
         torch.cuda.synchronize()
         exp, exp_inv = oracle.count_dense(data, idx, k)
         ok = np.array_equal(out.cpu().numpy(), exp) and np.array_equal(inv.cpu().numpy(), exp_inv)
-        print("case %2d: k=%2d %3d records %9d bytes %s" % (c, k, idx.size - 1, data.size, "ok" if ok else "MISMATCH"),
-              flush=True)
+        print("case %2d: k=%2d %3d records %9d bytes%s %s" % (c, k, idx.size - 1, data.size, mode,
+                                                            "ok" if ok else "MISMATCH"), flush=True)
+        if mode:
+            kmc.lib().kmc_diag_radix_mode(0, 1.0)
         bad += not ok
         del out, inv, d
     print("fuzz: %d/%d cases bit-exact" % (a.cases - bad, a.cases))
