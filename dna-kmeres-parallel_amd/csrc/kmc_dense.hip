@@ -22,8 +22,10 @@
 //            32-lane LDS group never collide on small alphabets (k <= 4: R = 32).
 //   k == 8 : 65 536 bins do not fit as 32-bit (256 KB > 160 KB LDS): two 16-bit
 //            counters per word (bin c in the low half, c|0x8000 in the high
-//            half).  ds_add_rtn reports the rare half-wrap; the lost 65 536 are
-//            recorded as a spill entry and re-added by spill_apply_kernel.
+//            half), plain adds; periodic scans move hot halves to spill entries,
+//            a piece whose halves wrapped anyway is recounted with returning adds
+//            (every wrap recorded as a spill entry), and reduce_dense_kernel adds
+//            the spill entries of every record back.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -523,9 +525,25 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     __shared__ uint32_t s_list[kRedList];
     __shared__ uint32_t s_n;
     __shared__ uint32_t s_part[RR][RW * NH];
+    __shared__ uint32_t s_out[RW * NH];
     const int tid = threadIdx.x, col = tid % RC, row = tid / RC;
     const int64_t c0 = (int64_t)blockIdx.x * RW;
     const Geom g = make_geom<Idx>(p);
+    // k = 8: the spill entries (halves moved out of 16-bit counters, wrap fix-ups)
+    // of record s that fall in this block's words, from the lists of the workgroups
+    // [wf, wlast] that hold its pieces; f(index into s_out layout, amount).  Only
+    // when one of those lists is non-empty (skewed input).
+    const auto for_spills = [&](int64_t s, int64_t wf, int64_t wlast, auto &&f) {
+        for (int64_t l = wf; l <= wlast; ++l) {
+            const uint32_t c = p.spill_cnt[l] < p.spill_cap ? p.spill_cnt[l] : p.spill_cap;
+            const Spill *sp = p.spill + l * (int64_t)p.spill_cap;
+            for (uint32_t i = tid; i < c; i += 256) {
+                const Spill e = sp[i];
+                const int64_t wd = (int64_t)(e.code & (NW - 1)) - c0;
+                if (e.rec == s && e.amount != 0 && wd >= 0 && wd < RW) f((int)wd + (e.code / NW) * RW, e.amount);
+            }
+        }
+    };
     for (int64_t s = blockIdx.y; s < p.n; s += gridDim.y) {
         int64_t ca, ce;
         record_windows<K, Idx>(p, g, s, ca, ce);
@@ -538,7 +556,19 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
         }
         const int64_t wf = ((ca >> kTileShift) - g.T0) / g.tpw;
         const int64_t wlast = (((ce - 1) >> kTileShift) - g.T0) / g.tpw;
-        if (wf == wlast) continue;  // written directly by the count kernel
+        bool spills = false;
+        if constexpr (P16) {
+            uint32_t any = 0u;
+            for (int64_t l = wf + tid; l <= wlast; l += 256) any |= p.spill_cnt[l];
+            spills = __syncthreads_or(any != 0u) != 0;
+        }
+        if (wf == wlast) {  // written directly by the count kernel: its spills on top
+            if (spills)
+                for_spills(s, wf, wlast, [&](int i, int32_t a) {
+                    atomicAdd(&p.sum[s + p.ld * (c0 + i % RW + (i / RW) * (int64_t)NW)], a);
+                });
+            continue;
+        }
         uint32_t acc[4 * NH] = {};
         for (int64_t cb = 2 * wf; cb <= 2 * wlast + 1; cb += kRedList) {
             const int64_t ce2 = (cb + kRedList) < (2 * wlast + 2) ? (cb + kRedList) : (2 * wlast + 2);
@@ -571,23 +601,21 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
             uint32_t t = 0u;
 #pragma unroll 8
             for (int r = 0; r < RR; ++r) t += s_part[r][i];
-            const int64_t c = c0 + i % RW + (i / RW) * NW;
-            p.sum[s + p.ld * c] = (int32_t)t;
+            s_out[i] = t;
         }
-        __syncthreads();  // s_part is reused by the next record
+        if (spills) {
+            __syncthreads();
+            for_spills(s, wf, wlast, [&](int i, int32_t a) { atomicAdd(&s_out[i], (uint32_t)a); });
+        }
+        __syncthreads();
+        for (int i = tid; i < RW * NH; i += 256) {
+            const int64_t c = c0 + i % RW + (i / RW) * NW;
+            p.sum[s + p.ld * c] = (int32_t)s_out[i];
+        }
+        __syncthreads();  // s_part and s_out are reused by the next record
     }
 }
 
-__global__ __launch_bounds__(256) void spill_apply_kernel(Params p) {
-    const int w = blockIdx.x;
-    uint32_t cnt = p.spill_cnt[w];
-    if (cnt > p.spill_cap) cnt = p.spill_cap;
-    const Spill *sp = p.spill + (int64_t)w * p.spill_cap;
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const Spill e = sp[i];
-        atomicAdd(&p.sum[e.rec + p.ld * (int64_t)e.code], e.amount);
-    }
-}
 
 // invalid[s] = (#windows of s in range) - sum over codes (the CPU path's bin 0);
 // records blockIdx.x, blockIdx.x + gridDim.x, ...
@@ -883,9 +911,8 @@ int run_dense(const Request &q, hipStream_t st) {
     he = hipGetLastError();
     if (he != hipSuccess) return (int)he;
     if (Cfg<K>::P16) {
-        hipLaunchKernelGGL(spill_apply_kernel, dim3(pl.G), dim3(256), 0, st, p);
-        he = hipGetLastError();
-        if (he != hipSuccess) return (int)he;
+        // (the spill entries are added by the reduce, which reads the lists of the
+        // workgroups that hold each record's pieces)
         // spill_cap_for bounds the entries a workgroup can emit (scan entries stand
         // for >= 32 768 windows, wrap entries for 65 536, at most 3 per wrap), and
         // p16_spill keeps counting past the cap; with KMC_CHECK_SPILL=1 (tests) the
