@@ -73,8 +73,6 @@ struct Params {
     Spill *spill;            // [G][spill_cap]
     uint32_t *spill_cnt;     // [G]
     uint32_t spill_cap;
-    uint64_t *fail_mask;     // [G] HM 3: bit i = i-th piece of the workgroup overflowed (bit 63: any >= 63)
-    int fallback;            // 1: recount only the pieces flagged in fail_mask (exact HM 1 kernel)
 };
 
 // 1 or 0x10000 from bit `hb` (0/1): one v_mad_u32_u24 (hipcc otherwise emits
@@ -345,6 +343,34 @@ struct DenseOp {
     }
 };
 
+// HM 3's exact recount of the windows [ps, pe) of a piece whose 16-bit halves
+// wrapped (skewed input only): returning adds, every wrap fixed up by p16_fix as
+// in HM 1, but a plain rolling-code walk over a contiguous run of windows per
+// thread, out of line -- the HM 1 tile stream inlined beside the hot loop made the
+// kernel spill VGPRs.  Bytes outside [rl, rh) are invalid, as in load_lane.
+template <int BLOCK>
+__device__ __noinline__ void recount_p16(const char *data, int64_t ps, int64_t pe, int64_t rl, int64_t rh,
+                                         const P16Ctx &pc) {
+    constexpr int K = 8;
+    const int64_t per = (pe - ps + BLOCK - 1) / BLOCK;
+    const int64_t i0 = ps + (int64_t)threadIdx.x * per;
+    const int64_t i1 = (i0 + per) < pe ? (i0 + per) : pe;
+    uint32_t code = 0u, run = 0u;
+    for (int64_t b = i0; b < i1 + K - 1; ++b) {
+        const uint32_t c = (b >= rl && b < rh) ? (uint32_t)(uint8_t)data[b] : 0u;
+        const uint32_t v = c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+        run = v < 4u ? run + 1u : 0u;
+        code = (code >> 2) | ((v & 3u) << (2 * K - 2));  // base b at bits 14..15 (LE order)
+        if (run >= (uint32_t)K) {                          // window b - K + 1 in [i0, i1)
+            const uint32_t word = code & 0x7FFFu, hb = code >> 15;
+            const uint32_t old = __hip_atomic_fetch_add(&pc.h[word], half_inc(hb), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t m = hb ? 0xFFFF0000u : 0x0000FFFFu;
+            if ((old & m) == m) p16_fix(pc, word, hb, old >= 0xFFFF0000u ? 1u : 0u);
+        }
+    }
+}
+
 template <int K, int R, int HM, class Idx, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     constexpr bool P16 = HM != 0;
@@ -366,11 +392,6 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     const int64_t tb = g.T0 + (int64_t)w * g.tpw;
     const int64_t te = (tb + g.tpw) < g.T1 ? (tb + g.tpw) : g.T1;
     int64_t slot0 = -1, slot1 = -1;
-    uint64_t redo = 0, failed = 0;
-    if (p.fallback) {
-        redo = p.fail_mask[w];
-        if (redo == 0) return;  // nothing of this workgroup overflowed (uniform)
-    }
 
     if (tb < te) {
         const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
@@ -385,8 +406,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                     else hi = mid - 1;
                 }
             }
-            // fallback launch: append to the first pass's spill entries
-            misc[0] = p.fallback ? p.spill_cnt[w] : 0u;
+            misc[0] = 0u;
             misc[3] = 0u;
             misc[4] = 0u;
             misc[5] = 0u;
@@ -397,7 +417,6 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
         __syncthreads();
         const int64_t s0 = (int64_t)((uint64_t)misc[1] | ((uint64_t)misc[2] << 32));
 
-        const uint32_t first_spills = misc[0];
         P16Ctx pc;
         pc.h = h;
         pc.spilled = misc + 5;
@@ -413,21 +432,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             const int64_t ps = ca > R0 ? ca : R0;
             const int64_t pe = ce < R1 ? ce : R1;
             if (ps >= pe) continue;
-            if (p.fallback) {  // recount only the flagged pieces (same piece numbering as the first pass)
-                const uint64_t bit = npieces < 63 ? (1ull << npieces) : (1ull << 63);
-                if ((redo & bit) == 0) {
-                    ++npieces;
-                    continue;
-                }
-            }
             pc.rec = s;
-            if (p.fallback && pc.spill) {
-                // the first pass's scan entries of this piece are superseded by the recount
-                const uint32_t nold = first_spills < pc.cap ? first_spills : pc.cap;
-                for (uint32_t i = tid; i < nold; i += BLOCK)
-                    if (pc.spill[i].rec == s) pc.spill[i].amount = 0;
-                __syncthreads();
-            }
             // this piece's tiles, split into contiguous per-wave runs
             const int64_t tp0 = ps >> kTileShift;
             const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
@@ -450,21 +455,51 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             }
             uint32_t *dst = p.slab + ((int64_t)w * 2 + slot) * NB;
             if constexpr (P16) {
-                uint32_t dsum = 0u;
-                for (int i = tid; i < NW; i += BLOCK) {
-                    const uint32_t v = h[i];
-                    h[i] = 0u;
-                    dsum += (v & 0xFFFFu) + (v >> 16);
-                    if (entire) {
-                        p.sum[s + p.ld * (int64_t)i] = (int32_t)(v & 0xFFFFu);
-                        p.sum[s + p.ld * (int64_t)(i + NW)] = (int32_t)(v >> 16);
-                    } else {
-                        dst[i] = v;  // packed as in LDS: the halves are exact (wraps live in spills)
+                // the packed words to sum[] (whole record) or the slab (packed as in
+                // LDS: the halves are exact, wraps live in spills); the LDS cleared
+                const auto flush = [&]() {
+                    uint32_t dsum = 0u;
+                    for (int i = tid; i < NW; i += BLOCK) {
+                        const uint32_t v = h[i];
+                        h[i] = 0u;
+                        dsum += (v & 0xFFFFu) + (v >> 16);
+                        if (entire) {
+                            p.sum[s + p.ld * (int64_t)i] = (int32_t)(v & 0xFFFFu);
+                            p.sum[s + p.ld * (int64_t)(i + NW)] = (int32_t)(v >> 16);
+                        } else {
+                            dst[i] = v;
+                        }
                     }
-                }
+                    return dsum;
+                };
+                const uint32_t dsum = flush();
                 if constexpr (HM == 3) {
                     const uint32_t wsum = wave_sum(dsum);
                     if (lane == 0) atomicAdd(&misc[4], wsum);
+                    // every 16-bit wrap only loses counts (low half: -65535 net, high
+                    // half: -65536), so the decoded total plus the scans' spills equals
+                    // the windows added iff none wrapped
+                    __syncthreads();
+                    if (tid == 0) {
+                        misc[6] = misc[3] != misc[4] + misc[5] ? 1u : 0u;
+                        misc[3] = 0u;
+                        misc[4] = 0u;
+                        misc[5] = 0u;
+                    }
+                    __syncthreads();
+                    if (misc[6]) {
+                        // a half wrapped (skewed input): recount the piece exactly with
+                        // returning adds (HM 1), in place of a second launch; its scan
+                        // entries are superseded (zeroed), the recount's wrap entries
+                        // appended after them
+                        const uint32_t n0 = misc[0] < pc.cap ? misc[0] : pc.cap;
+                        for (uint32_t i = tid; i < n0; i += BLOCK)
+                            if (pc.spill[i].rec == s) pc.spill[i].amount = 0;
+                        __syncthreads();
+                        recount_p16<BLOCK>(p.data, ps, pe, g.rl, g.rh, pc);
+                        __syncthreads();
+                        (void)flush();
+                    }
                 }
             } else {
                 for (int c = tid; c < NB; c += BLOCK) {
@@ -479,27 +514,12 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 }
             }
             __syncthreads();
-            if constexpr (HM == 3) {
-                // every 16-bit wrap only loses counts (low half: -65535 net, high half:
-                // -65536), so the decoded total plus the scans' spills equals the
-                // windows added iff none wrapped
-                if (tid == 0) {
-                    if (misc[3] != misc[4] + misc[5]) failed |= npieces < 63 ? (1ull << npieces) : (1ull << 63);
-                    misc[3] = 0u;
-                    misc[4] = 0u;
-                    misc[5] = 0u;
-                }
-                __syncthreads();
-            }
             ++npieces;
         }
     }
     if (tid == 0) {
-        if (!p.fallback) {
-            p.slot_rec[2 * w] = slot0;
-            p.slot_rec[2 * w + 1] = slot1;
-        }
-        if (HM == 3) p.fail_mask[w] = failed;
+        p.slot_rec[2 * w] = slot0;
+        p.slot_rec[2 * w + 1] = slot1;
         if (p.spill_cnt) p.spill_cnt[w] = (tb < te) ? misc[0] : 0u;
     }
 }
@@ -727,7 +747,7 @@ bool check_spill() {
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct WsLayout {
-    size_t slot_rec, spill_cnt, fail_mask, slab, spill, total;
+    size_t slot_rec, spill_cnt, slab, spill, total;
 };
 
 inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
@@ -738,8 +758,6 @@ inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
     o += align256((size_t)G * 2 * sizeof(int64_t));
     L.spill_cnt = o;
     o += align256((size_t)G * sizeof(uint32_t));
-    L.fail_mask = o;
-    o += align256((size_t)G * sizeof(uint64_t));
     L.slab = o;
     o += align256((size_t)G * 2 * nb * sizeof(uint32_t));
     L.spill = o;
@@ -877,8 +895,6 @@ int run_dense(const Request &q, hipStream_t st) {
     p.slab = reinterpret_cast<uint32_t *>(base + pl.L.slab);
     p.spill = Cfg<K>::P16 ? reinterpret_cast<Spill *>(base + pl.L.spill) : nullptr;
     p.spill_cap = pl.spill_cap;
-    p.fail_mask = reinterpret_cast<uint64_t *>(base + pl.L.fail_mask);
-    p.fallback = 0;
 
     constexpr int NB = 1 << (2 * K);
     if (t_trace_before) {
@@ -893,16 +909,8 @@ int run_dense(const Request &q, hipStream_t st) {
         he = hipEventRecord(t_trace_after, st);
         if (he != hipSuccess) return (int)he;
     }
-    if constexpr (Cfg<K>::HM == 3) {
-        // exact recount of the pieces whose 16-bit counters wrapped (skewed input);
-        // workgroups with nothing flagged exit at once
-        Params pf = p;
-        pf.fallback = 1;
-        hipLaunchKernelGGL((count_dense_kernel<K, Cfg<K>::R, 1, Idx, Cfg<K>::BLOCK>), dim3(pl.G),
-                           dim3(Cfg<K>::BLOCK), 0, st, pf);
-        he = hipGetLastError();
-        if (he != hipSuccess) return (int)he;
-    }
+    // (HM 3: pieces whose 16-bit counters wrapped are recounted by the count kernel
+    // itself, right after their flush)
     constexpr int NWR = Cfg<K>::P16 ? NB / 2 : NB;  // slab words per slot
     constexpr int RW = NWR / 4 < 16 ? NWR : 64;      // words per reduce block (its RW)
     const unsigned cb = (unsigned)(NWR / RW);
