@@ -527,13 +527,15 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
 // Records that span several workgroups: sum their slab slots; records without a
 // window in range get zeros.  Grid (NW / RW, ny): blockIdx.x picks RW = 4 * RC
 // slab words (NW = 4^k words, or 4^k / 2 packed words at k = 8, each holding bins
-// c and c | 0x8000), records s = blockIdx.y, blockIdx.y + ny, ...  The block first
-// lists the record's slots (slot_rec, in LDS), then RC columns of 16-byte loads x
-// RR rows of slots sum them with no dependent load in the loop, and the rows meet
-// in LDS.  (One thread per word walking the workgroups with a slot_rec test before
-// every slab load was latency-bound: 72 us for the ~205 slots of an 8-way shard's
-// record, against a 325 us histogram; scripts/shardbench.py.)
-constexpr int kRedList = 1024;  // slot candidates listed per chunk
+// c and c | 0x8000), records s = blockIdx.y, blockIdx.y + ny, ...  RC columns of
+// 16-byte loads x RR rows of slots sum a record's slots with no dependent load in
+// the loop, and the rows meet in LDS.  The slots follow from the geometry: record s
+// spans workgroups wf < wlast, each of wf + 1 .. wlast holds it as its first piece
+// (slot 0: its range starts inside s), and wf in slot 0 or 1 as slot_rec says.
+// (One thread per word walking the workgroups with a slot_rec test before every
+// slab load was latency-bound: 72 us for the ~205 slots of an 8-way shard's
+// record, against a 325 us histogram; listing the slots from slot_rec in LDS first
+// cost a round trip and two barriers per record.)
 template <int K, class Idx, bool P16>
 __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     constexpr int NB = 1 << (2 * K);
@@ -542,8 +544,6 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     constexpr int RR = 256 / RC;                   // rows over the slots
     constexpr int RW = 4 * RC;                     // words per block
     constexpr int NH = P16 ? 2 : 1;                // counters per word
-    __shared__ uint32_t s_list[kRedList];
-    __shared__ uint32_t s_n;
     __shared__ uint32_t s_part[RR][RW * NH];
     __shared__ uint32_t s_out[RW * NH];
     const int tid = threadIdx.x, col = tid % RC, row = tid / RC;
@@ -590,27 +590,21 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
             continue;
         }
         uint32_t acc[4 * NH] = {};
-        for (int64_t cb = 2 * wf; cb <= 2 * wlast + 1; cb += kRedList) {
-            const int64_t ce2 = (cb + kRedList) < (2 * wlast + 2) ? (cb + kRedList) : (2 * wlast + 2);
-            __syncthreads();  // the previous chunk's list is consumed
-            if (tid == 0) s_n = 0u;
-            __syncthreads();
-            for (int64_t j = cb + tid; j < ce2; j += 256)
-                if (p.slot_rec[j] == s) s_list[atomicAdd(&s_n, 1u)] = (uint32_t)(j - cb);
-            __syncthreads();
-            const uint32_t n = s_n;
+        // slot of workgroup wf + i: 2 (wf + i) for i > 0; wf's first or second
+        const int64_t sf = 2 * wf + (p.slot_rec[2 * wf] == s ? 0 : 1);
+        const int64_t n = wlast - wf + 1;
 #pragma unroll 4
-            for (uint32_t i = row; i < n; i += RR) {
-                const uint4 v = reinterpret_cast<const uint4 *>(p.slab + (cb + s_list[i]) * NB + c0)[col];
-                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+        for (int64_t i = row; i < n; i += RR) {
+            const int64_t slot = i == 0 ? sf : 2 * (wf + i);
+            const uint4 v = reinterpret_cast<const uint4 *>(p.slab + slot * NB + c0)[col];
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if constexpr (P16) {
-                        acc[e] += x[e] & 0xFFFFu;  // bin c
-                        acc[4 + e] += x[e] >> 16;  // bin c + NW
-                    } else {
-                        acc[e] += x[e];
-                    }
+            for (int e = 0; e < 4; ++e) {
+                if constexpr (P16) {
+                    acc[e] += x[e] & 0xFFFFu;  // bin c
+                    acc[4 + e] += x[e] >> 16;  // bin c + NW
+                } else {
+                    acc[e] += x[e];
                 }
             }
         }
