@@ -241,6 +241,25 @@ def test_radix_sampled_regions_vs_oracle(kmc, oracle, cuda, radix_mode, k, scale
     np.testing.assert_array_equal(inv, exp_inv)
 
 
+@pytest.mark.parametrize("k", [10, 13])
+def test_radix_sampled_long_list(kmc, oracle, cuda, radix_mode, k):
+    """Sampled partition with one very long list: a bucket taking a 5 Mbase poly-A
+    run (one region per workgroup holding it, its bins wrapping: R4's exact
+    recount of the regions), beside random records."""
+    assert radix_mode(2, 1.0) == 0
+    rng = np.random.default_rng(8100 + k)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    recs = [np.concatenate([acgt[rng.integers(0, 4, 700_000)], np.full(5_000_000, ord("A"), np.uint8),
+                            acgt[rng.integers(0, 4, 300_001)], [0]]).astype(np.uint8),
+            np.append(acgt[rng.integers(0, 4, 2_000_000)], np.uint8(0))]
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+
+
 @pytest.mark.parametrize("scale", [1.0, 0.5])
 def test_radix_sampled_shards_and_workspace(kmc, oracle, cuda, radix_mode, scale):
     """Sampled partition over byte-range shards (window range + halo) with a caller
