@@ -722,7 +722,11 @@ __device__ __forceinline__ void hist_regions(const uint16_t *ent, const uint32_t
             if (j < V) {
                 while (j >= ve) enter(++r);
                 const unsigned long long va = va0 + (j - vb);
-                x[u] = v[va];
+                // non-temporal: the entries are read once (C3's R4 4.95 -> 4.52 ms, same
+                // box; with eight loads in flight per lane instead of four: 4.60)
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(v + va));
+                x[u] = make_uint4(t[0], t[1], t[2], t[3]);
                 if (j >= jf && j < jl) {
                     m[u] = 0xFFu;
                 } else {  // a region's first or last vector: entries [lo, lo + rn) of it
