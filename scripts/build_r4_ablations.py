@@ -4,13 +4,14 @@ from patched copies of csrc/kmc_radix.hip outside the tree (/tmp/r4abl/<tag>), l
 with the in-tree objects into dna-kmeres-parallel_amd/lib/variants/libkmc_r4abl_<tag>.so,
 for scripts/gpu_r03u.sh / gpu_r03v.sh / gpu_r03w.sh.  The
 "noadd" and "noload" variants count wrongly by construction; "wave", "nt", "u8" and
-"nt_u8" are correct alternatives.  The patches apply to kmc_radix.hip as of commit
+"nt_u8" are correct alternatives, as are "exact_nt" and "place_nt" (which apply to
+the shipped source: R4ABL_REV=HEAD).  The patches apply to kmc_radix.hip as of commit
 3306378 (before the shipped non-temporal loads), read with `git show`.  Run
 `make -C dna-kmeres-parallel_amd` first (the other objects are linked from build/).
 Usage: python scripts/build_r4_ablations.py [tag ...]   (default: all)"""
 import os, subprocess, sys
 R = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dna-kmeres-parallel_amd")
-SRC_REV = "3306378"
+SRC_REV = os.environ.get("R4ABL_REV", "3306378")
 src = subprocess.check_output(["git", "-C", R, "show", SRC_REV + ":dna-kmeres-parallel_amd/csrc/kmc_radix.hip"], text=True)
 def variant(tag, reps):
     s = src
@@ -63,7 +64,18 @@ nt = [("""                x[u] = v[va];""", """                {
                 }""")]
 u8 = [("#define KMC_R4_U 4  //", "#define KMC_R4_U 8  //")]
 
-VARIANTS = {"noadd": noadd, "noload": noload, "wave": wave, "wave_noadd": wave + noadd, "nt": nt, "u8": u8,
+# on the shipped source (R4ABL_REV=HEAD): the exact walk's loads and R5's stage reads non-temporal
+exact_nt = [("        const auto ld = [&](uint64_t k) { return v[k]; };",
+             """        const auto ld = [&](uint64_t k) {
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(v + k));
+            return make_uint4(t[0], t[1], t[2], t[3]);
+        };""")]
+place_nt = [("            const uint4 v = *reinterpret_cast<const uint4 *>(p.stage + (s0 + r) * nbins + c0 + cc);",
+             """            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 t4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p.stage + (s0 + r) * nbins + c0 + cc));
+            const uint4 v = make_uint4(t4[0], t4[1], t4[2], t4[3]);""")]
+VARIANTS = {"exact_nt": exact_nt, "place_nt": place_nt, "noadd": noadd, "noload": noload, "wave": wave, "wave_noadd": wave + noadd, "nt": nt, "u8": u8,
             "nt_u8": nt + u8}
 if __name__ == "__main__":
     for tag in sys.argv[1:] or list(VARIANTS):
