@@ -376,6 +376,8 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     kmc.trace_events(None, None)
+    if kmc.lib().kmc_dense_status(local) != 0:  # a k = 8 spill list overflowed (never expected)
+        raise SystemExit("count check failed: kmc_dense_status reports a spill overflow")
     # algorithmic bytes of one histogram launch on this GPU: its ASCII input bytes +
     # the int32 matrix it writes
     alg_bytes = (win_hi - win_lo) + 4 * nb * n_tot

@@ -73,6 +73,7 @@ struct Params {
     Spill *spill;            // [G][spill_cap]
     uint32_t *spill_cnt;     // [G]
     uint32_t spill_cap;
+    uint32_t *status;        // host-mapped flag (kmc_dense_status): a workgroup overflowed its spill list
 };
 
 // 1 or 0x10000 from bit `hb` (0/1): one v_mad_u32_u24 (hipcc otherwise emits
@@ -163,67 +164,9 @@ __device__ __forceinline__ void count_tile32(uint32_t lo, uint32_t hi, uint32_t 
     add32<K, R, 15, MASKED>(lo, mid, W, h, rep);
 }
 
-// k == 8, packed 16-bit halves with returning adds (HM == 1).  The 16 adds of a
-// tile are issued, and their returned values are checked one tile later
-// (p16_check), so the LDS return latency hides behind the next tile's decode.
-struct P16Pending {
-    uint32_t old[16];
-    uint32_t lo, hi, W;
-};
-
-template <bool MASKED>
-__device__ __forceinline__ void count_tile_p16(uint32_t lo, uint32_t hi, uint32_t W, const P16Ctx &pc,
-                                               P16Pending &pd) {
-    const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t src = (j <= 8) ? lo : mid;
-        const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
-        const uint32_t word = (src >> off) & 0x7FFFu;
-        const uint32_t hb = (src >> (off + 15)) & 1u;
-        pd.old[j] = 0u;
-        if (!MASKED || ((W >> j) & 1u))
-            pd.old[j] = __hip_atomic_fetch_add(&pc.h[word], half_inc(hb), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    pd.lo = lo;
-    pd.hi = hi;
-    pd.W = MASKED ? W : 0xFFFFu;
-}
-
-// Conservative precheck: a half can only have wrapped if some returned value had
-// a half >= 0x8000; random input never gets there, skewed input takes the exact
-// per-window path.
-__device__ __forceinline__ void p16_check(const P16Ctx &pc, const P16Pending &pd) {
-    uint32_t any = 0u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) any |= pd.old[j];
-    if (__any((any & 0x80008000u) != 0u)) {
-        const uint32_t mid = __builtin_amdgcn_alignbit(pd.hi, pd.lo, 16);
-        uint32_t ovf = 0u, hw = 0u;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t src = (j <= 8) ? pd.lo : mid;
-            const int off = (j <= 8) ? 2 * j : 2 * (j - 8);
-            const uint32_t m = ((src >> (off + 15)) & 1u) ? 0xFFFF0000u : 0x0000FFFFu;
-            ovf |= (uint32_t)((pd.old[j] & m) == m) << j;
-            hw |= (uint32_t)(pd.old[j] >= 0xFFFF0000u) << j;
-        }
-        ovf &= pd.W;
-        if (ovf != 0u) {
-            const uint64_t both = (uint64_t)pd.lo | ((uint64_t)pd.hi << 32);
-            for (int j = 0; j < 16; ++j) {
-                if ((ovf >> j) & 1u) {
-                    const uint32_t code = (uint32_t)(both >> (2 * j)) & 0xFFFFu;
-                    p16_fix(pc, code & 0x7FFFu, code >> 15, (hw >> j) & 1u);
-                }
-            }
-        }
-    }
-}
-
-// k == 8, packed 16-bit halves, plain adds (HM == 2): overflow is excluded by the
-// between-barrier scans of count_wave_range (p16_scan).
+// k == 8, packed 16-bit halves, plain adds (HM == 3): a half that reaches 32 768
+// is moved to a spill entry by the periodic scans (p16_scan), a wrap between two
+// scans is detected by the piece total and the piece recounted (recount_p16).
 template <bool MASKED>
 __device__ __forceinline__ void count_tile_p16_plain(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h) {
     const uint32_t mid = __builtin_amdgcn_alignbit(hi, lo, 16);
@@ -239,24 +182,12 @@ __device__ __forceinline__ void count_tile_p16_plain(uint32_t lo, uint32_t hi, u
 }
 
 template <int K, int R, int HM, bool MASKED>
-__device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h, int lane,
-                                           const P16Ctx &pc, P16Pending &pd) {
-    if constexpr (HM == 1)
-        count_tile_p16<MASKED>(lo, hi, W, pc, pd);
-    else if constexpr (HM == 2 || HM == 3)
+__device__ __forceinline__ void count_tile(uint32_t lo, uint32_t hi, uint32_t W, uint32_t *h, int lane) {
+    if constexpr (HM == 3)
         count_tile_p16_plain<MASKED>(lo, hi, W, h);
     else
         count_tile32<K, R, MASKED>(lo, hi, W, h, lane);
 }
-
-// HM == 2 overflow scans.  Between two scans the workgroup adds at most
-// NWAVES*ScanTiles<BLOCK>*1024 windows (each wave ScanTiles tiles); a scan moves
-// every 16-bit half >= T down to (half mod T), the rest going to a spill entry.
-// With NWAVES*ScanTiles*1024 <= 65536 - T a half is < T after a scan and
-// <= 65535 before the next one: no half ever wraps.
-template <int BLOCK> struct Scan;
-template <> struct Scan<1024> { static constexpr int kTiles = 3; static constexpr uint32_t kT = 16384; };
-template <> struct Scan<512> { static constexpr int kTiles = 7; static constexpr uint32_t kT = 8192; };
 
 // Cold path of the scan: move every half's multiple of T of 4 words into spills.
 template <uint32_t T>
@@ -295,33 +226,25 @@ __device__ __forceinline__ void p16_scan(const P16Ctx &pc) {
     }
 }
 
-// The dense histogram as a stream_tiles operation (one per histogram mode).
+// The dense histogram as a stream_tiles operation (HM 0: 32-bit bins, HM 3: k = 8
+// packed 16-bit halves).
 template <int K, int R, int HM, int BLOCK>
 struct DenseOp {
+    static_assert(HM == 0 || HM == 3, "histogram modes: 0 (32-bit bins) and 3 (k = 8 packed halves)");
     uint32_t *h;
     int lane;
     const P16Ctx &pc;
-    P16Pending pd;
-    bool pending = false;
     uint32_t nwin = 0u;  // HM 3: windows this lane added
 
     __device__ DenseOp(uint32_t *h_, int lane_, const P16Ctx &pc_) : h(h_), lane(lane_), pc(pc_) {}
 
-    __device__ __forceinline__ void before_tile() {
-        if constexpr (HM == 1) {
-            if (pending) p16_check(pc, pd);
-        }
-    }
+    __device__ __forceinline__ void before_tile() {}
     template <bool MASKED>
     __device__ __forceinline__ void tile(uint32_t lo, uint32_t hi, uint32_t W) {
-        count_tile<K, R, HM, MASKED>(lo, hi, W, h, lane, pc, pd);
-        if constexpr (HM == 1) pending = true;
+        count_tile<K, R, HM, MASKED>(lo, hi, W, h, lane);
         if constexpr (HM == 3) nwin += MASKED ? (uint32_t)__builtin_popcount(W) : 16u;
     }
     __device__ __forceinline__ void after_iter(int64_t i, int64_t per, bool) {
-        if constexpr (HM == 1) {
-            if (pending && i + 1 == per) p16_check(pc, pd);
-        }
         if constexpr (HM == 3 && KMC_HM3_SCAN > 0) {
             // hot halves (>= 32768) go to spill entries every KMC_HM3_SCAN tiles per
             // wave, so a half wraps only if one k-mer takes >= 32768 of the
@@ -333,21 +256,14 @@ struct DenseOp {
                 lds_barrier();
             }
         }
-        if constexpr (HM == 2) {
-            if ((i % Scan<BLOCK>::kTiles) == Scan<BLOCK>::kTiles - 1 && i + 1 < per) {
-                lds_barrier();
-                p16_scan<BLOCK, Scan<BLOCK>::kT>(pc);
-                lds_barrier();
-            }
-        }
     }
 };
 
 // HM 3's exact recount of the windows [ps, pe) of a piece whose 16-bit halves
-// wrapped (skewed input only): returning adds, every wrap fixed up by p16_fix as
-// in HM 1, but a plain rolling-code walk over a contiguous run of windows per
-// thread, out of line -- the HM 1 tile stream inlined beside the hot loop made the
-// kernel spill VGPRs.  Bytes outside [rl, rh) are invalid, as in load_lane.
+// wrapped (skewed input only): returning adds, every wrap fixed up by p16_fix, over
+// a plain rolling-code walk of a contiguous run of windows per thread, out of line
+// (a returning-add tile stream inlined beside the hot loop made the kernel spill
+// VGPRs).  Bytes outside [rl, rh) are invalid, as in load_lane.
 template <int BLOCK>
 __device__ __noinline__ void recount_p16(const char *data, int64_t ps, int64_t pe, int64_t rl, int64_t rh,
                                          const P16Ctx &pc) {
@@ -374,8 +290,6 @@ __device__ __noinline__ void recount_p16(const char *data, int64_t ps, int64_t p
 template <int K, int R, int HM, class Idx, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     constexpr bool P16 = HM != 0;
-    static_assert(HM != 2 || (BLOCK / 64) * Scan<BLOCK>::kTiles * kTile + Scan<BLOCK>::kT <= 65536,
-                  "scan interval bound");
     constexpr int NB = 1 << (2 * K);
     constexpr int NW = P16 ? NB / 2 : NB * R;
     constexpr int NWAVES = BLOCK / 64;
@@ -489,7 +403,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                     __syncthreads();
                     if (misc[6]) {
                         // a half wrapped (skewed input): recount the piece exactly with
-                        // returning adds (HM 1), in place of a second launch; its scan
+                        // returning adds, in place of a second launch; its scan
                         // entries are superseded (zeroed), the recount's wrap entries
                         // appended after them
                         const uint32_t n0 = misc[0] < pc.cap ? misc[0] : pc.cap;
@@ -520,7 +434,13 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     if (tid == 0) {
         p.slot_rec[2 * w] = slot0;
         p.slot_rec[2 * w + 1] = slot1;
-        if (p.spill_cnt) p.spill_cnt[w] = (tb < te) ? misc[0] : 0u;
+        if (p.spill_cnt) {
+            p.spill_cnt[w] = (tb < te) ? misc[0] : 0u;
+            // never expected (spill_cap_for bounds the entries), but a lost entry
+            // would be a silent short count: raise the deferred status flag
+            if (tb < te && misc[0] > p.spill_cap && p.status)
+                __hip_atomic_store(p.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -552,15 +472,25 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     // k = 8: the spill entries (halves moved out of 16-bit counters, wrap fix-ups)
     // of record s that fall in this block's words, from the lists of the workgroups
     // [wf, wlast] that hold its pieces; f(index into s_out layout, amount).  Only
-    // when one of those lists is non-empty (skewed input).
+    // when one of those lists is non-empty (skewed input).  A workgroup walks its
+    // pieces in record order and appends a piece's entries before the next piece
+    // starts, so every list is sorted by rec: a binary search finds s's entries,
+    // and a list holding many records' entries costs each record only its own.
     const auto for_spills = [&](int64_t s, int64_t wf, int64_t wlast, auto &&f) {
         for (int64_t l = wf; l <= wlast; ++l) {
             const uint32_t c = p.spill_cnt[l] < p.spill_cap ? p.spill_cnt[l] : p.spill_cap;
             const Spill *sp = p.spill + l * (int64_t)p.spill_cap;
-            for (uint32_t i = tid; i < c; i += 256) {
+            uint32_t lo = 0u, hi = c;  // first entry with rec >= s (wave-uniform search)
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (sp[mid].rec < s) lo = mid + 1u;
+                else hi = mid;
+            }
+            for (uint32_t i = lo + tid; i < c; i += 256) {
                 const Spill e = sp[i];
+                if (e.rec != s) break;
                 const int64_t wd = (int64_t)(e.code & (NW - 1)) - c0;
-                if (e.rec == s && e.amount != 0 && wd >= 0 && wd < RW) f((int)wd + (e.code / NW) * RW, e.amount);
+                if (e.amount != 0 && wd >= 0 && wd < RW) f((int)wd + (e.code / NW) * RW, e.amount);
             }
         }
     };
@@ -663,13 +593,10 @@ __global__ __launch_bounds__(256) void invalid_kernel(Params p) {
 template <int K>
 struct Cfg;
 // R = replicas of each 32-bit bin; BLOCK = threads per workgroup
-// HM = histogram mode: 0 = 32-bit bins; k == 8 packed 16-bit halves with
-//   1 = returning adds + exact wrap fix-up, 2 = plain adds + overflow scans,
-//   3 = plain adds + wrap detection by total, pieces that wrapped recounted with 1.
-// KMC_K8_MODE selects the k == 8 mode (diagnostic builds compare them).
-#ifndef KMC_K8_MODE
-#define KMC_K8_MODE 3
-#endif
+// HM = histogram mode: 0 = 32-bit bins; 3 = k == 8 packed 16-bit halves, plain adds
+//   + periodic hot-half scans + wrap detection by total, pieces that wrapped
+//   recounted with returning adds (round 1 also had returning adds throughout and
+//   scans every 3 tiles as modes 1 and 2; both measured slower and were removed).
 template <> struct Cfg<1> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<2> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<3> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
@@ -686,11 +613,13 @@ template <> struct Cfg<7> { static constexpr int R = 1, BLOCK = 512, HM = 0; sta
 #ifndef KMC_K8_BLOCK
 #define KMC_K8_BLOCK 1024
 #endif
-template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = KMC_K8_BLOCK, HM = KMC_K8_MODE; static constexpr bool P16 = true; };
+template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = KMC_K8_BLOCK, HM = 3; static constexpr bool P16 = true; };
 
 struct DevInfo {
     int cus = 0;
     int occ[KMC_DENSE_MAX_K + 1][2] = {};  // [k][idx64]
+    uint32_t *status_host = nullptr;       // kmc_dense_status flag (host-mapped, allocated on first use)
+    uint32_t *status_dev = nullptr;
 };
 
 std::mutex g_mu;
@@ -702,8 +631,13 @@ void *kernel_ptr() {
     return reinterpret_cast<void *>(&count_dense_kernel<K, Cfg<K>::R, Cfg<K>::HM, Idx, Cfg<K>::BLOCK>);
 }
 
-// CUs left out of the dense grid (kmc_set_reserved_cus)
-std::atomic<int> g_reserved_cus{0};
+// CUs left out of the dense grid (kmc_set_reserved_cus), per host thread
+thread_local int t_reserved_cus = 0;
+
+#ifdef KMC_DIAG_HOOKS
+// test hook (diagnostic library only): spill list capacity per workgroup (0: the bound)
+std::atomic<uint32_t> g_diag_spill_cap{0};
+#endif
 
 template <int K, class Idx>
 int grid_size(int device, int &G) {
@@ -725,17 +659,45 @@ int grid_size(int device, int &G) {
         d.occ[K][ix] = nb > 0 ? nb : 1;
     }
     // kmc_set_reserved_cus: leave that many CUs to a concurrent kernel
-    const int cus = d.cus - g_reserved_cus.load(std::memory_order_relaxed);
+    const int cus = d.cus - t_reserved_cus;
     G = (cus > 0 ? cus : 1) * d.occ[K][ix];
     return 0;
 }
 
-bool check_spill() {
-    static const bool on = [] {
-        const char *e = std::getenv("KMC_CHECK_SPILL");
-        return e != nullptr && e[0] == '1';
-    }();
-    return on;
+// The device's kmc_dense_status flag: host-mapped, written by the k = 8 kernel.
+int status_flag(int device, uint32_t **host, uint32_t **dev) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((int)g_dev.size() <= device) g_dev.resize(device + 1);
+    DevInfo &d = g_dev[device];
+    if (!d.status_host) {
+        void *h = nullptr;
+        hipError_t e = hipHostMalloc(&h, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) return KMC_ERR_NOMEM;
+        void *dp = nullptr;
+        e = hipHostGetDevicePointer(&dp, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            return (int)e;
+        }
+        *static_cast<volatile uint32_t *>(h) = 0u;
+        d.status_host = static_cast<uint32_t *>(h);
+        d.status_dev = static_cast<uint32_t *>(dp);
+    }
+    *host = d.status_host;
+    *dev = d.status_dev;
+    return 0;
+}
+
+// Read and clear the flag of `device` (no device call).
+int take_status(int device) {
+    uint32_t *h = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if ((int)g_dev.size() > device && device >= 0) h = g_dev[device].status_host;
+    }
+    if (!h) return KMC_OK;
+    const uint32_t v = __atomic_exchange_n(h, 0u, __ATOMIC_ACQ_REL);
+    return v ? KMC_ERR_CAPACITY : KMC_OK;
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -793,7 +755,13 @@ int make_plan(int device, bool derive, int64_t wl, int64_t wh, Plan &pl) {
         const int64_t tiles = wh > wl ? ((wh + kTile - 1) >> kTileShift) - (wl >> kTileShift) : 0;
         if (tiles < G) G = tiles > 0 ? (int)tiles : 1;
         const int64_t tpw = tiles > 0 ? (tiles + G - 1) / G : 1;
-        if (Cfg<K>::P16) pl.spill_cap = spill_cap_for(tpw);
+        if (Cfg<K>::P16) {
+            pl.spill_cap = spill_cap_for(tpw);
+#ifdef KMC_DIAG_HOOKS
+            const uint32_t dc = g_diag_spill_cap.load();
+            if (dc) pl.spill_cap = dc;
+#endif
+        }
     }
     pl.G = G;
     pl.L = ws_layout(K, G, pl.spill_cap);
@@ -889,6 +857,12 @@ int run_dense(const Request &q, hipStream_t st) {
     p.slab = reinterpret_cast<uint32_t *>(base + pl.L.slab);
     p.spill = Cfg<K>::P16 ? reinterpret_cast<Spill *>(base + pl.L.spill) : nullptr;
     p.spill_cap = pl.spill_cap;
+    p.status = nullptr;
+    if (Cfg<K>::P16) {
+        uint32_t *sh = nullptr;
+        e = status_flag(device, &sh, &p.status);
+        if (e) return e;
+    }
 
     constexpr int NB = 1 << (2 * K);
     if (t_trace_before) {
@@ -912,22 +886,12 @@ int run_dense(const Request &q, hipStream_t st) {
                        dim3(256), 0, st, p);
     he = hipGetLastError();
     if (he != hipSuccess) return (int)he;
-    if (Cfg<K>::P16) {
-        // (the spill entries are added by the reduce, which reads the lists of the
-        // workgroups that hold each record's pieces)
-        // spill_cap_for bounds the entries a workgroup can emit (scan entries stand
-        // for >= 32 768 windows, wrap entries for 65 536, at most 3 per wrap), and
-        // p16_spill keeps counting past the cap; with KMC_CHECK_SPILL=1 (tests) the
-        // call synchronises and fails instead of returning counts that lost entries
-        if (check_spill()) {
-            std::vector<uint32_t> cnt(pl.G);
-            he = hipMemcpyAsync(cnt.data(), p.spill_cnt, pl.G * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
-            if (he == hipSuccess) he = hipStreamSynchronize(st);
-            if (he != hipSuccess) return (int)he;
-            for (uint32_t c : cnt)
-                if (c > pl.spill_cap) return KMC_ERR_CAPACITY;
-        }
-    }
+    // (k = 8: the spill entries are added by the reduce, which reads the lists of
+    // the workgroups that hold each record's pieces.  spill_cap_for bounds the
+    // entries a workgroup can emit -- scan entries stand for >= 32 768 windows, wrap
+    // entries for 65 536, at most 3 per wrap -- and p16_spill keeps counting past
+    // the cap, so an overflow raises the kmc_dense_status flag instead of passing
+    // silently.)
     if (q.invalid) {
         hipLaunchKernelGGL((invalid_kernel<K, Idx>), dim3((unsigned)std::min<int64_t>(q.n, kMaxGridX)), dim3(256), 0,
                            st, p);
@@ -977,9 +941,20 @@ using namespace kmc;
 
 extern "C" int kmc_set_reserved_cus(int n) {
     if (n < 0 || n > 64) return KMC_ERR_INVALID_ARG;
-    g_reserved_cus.store(n, std::memory_order_relaxed);
+    t_reserved_cus = n;
     return KMC_OK;
 }
+
+extern "C" int kmc_dense_status(int device) { return take_status(device); }
+
+#ifdef KMC_DIAG_HOOKS
+// Test hook (diagnostic library only, not in kmc.h): the k = 8 spill list
+// capacity per workgroup, lowered so that an overflow raises the status flag.
+extern "C" KMC_DIAG_API int kmc_diag_dense_spill_cap(unsigned cap) {
+    g_diag_spill_cap.store(cap);
+    return KMC_OK;
+}
+#endif
 
 extern "C" int kmc_trace_set_events(hipEvent_t before, hipEvent_t after) {
     t_trace_before = before;
@@ -1003,6 +978,8 @@ extern "C" int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, un
     q.sum = sum;
     q.ld = num_seqs;
     q.derive = true;
+    int device = 0;
+    if (hipGetDevice(&device) == hipSuccess && take_status(device) != KMC_OK) return KMC_ERR_CAPACITY;
     return dispatch<int>(KMC_DROPIN_K, q, stream);
 }
 
@@ -1040,6 +1017,10 @@ extern "C" int kmc_count_dense_ex(const kmc_dense_args *a0, hipStream_t stream) 
     if (!a0->data || !a0->indices || !a0->sum) return KMC_ERR_INVALID_ARG;
     if (a0->read_hi < a0->read_lo || a0->win_hi < a0->win_lo) return KMC_ERR_INVALID_ARG;
     if (a0->sum_ld != 0 && a0->sum_ld < a0->num_seqs) return KMC_ERR_INVALID_ARG;
+    {  // a deferred overflow of an earlier call on this device is reported now
+        int device = 0;
+        if (hipGetDevice(&device) == hipSuccess && take_status(device) != KMC_OK) return KMC_ERR_CAPACITY;
+    }
     int64_t bias = 0;
     const kmc_dense_args al = aligned_args(a0, bias);
     const kmc_dense_args *a = &al;

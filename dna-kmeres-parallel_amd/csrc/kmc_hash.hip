@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "kmc.h"
+#include "kmc_internal.h"
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
@@ -1171,62 +1172,54 @@ inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 using namespace kmc;
 
-// Test hook (not in kmc.h): K4's per-wave claim capacity, lowered so that the
+#ifdef KMC_DIAG_HOOKS
+// Test hook (diagnostic library only, not in kmc.h): K4's per-wave claim capacity, lowered so that the
 // pass-overflow split runs often; 0 restores the default.
-extern "C" int kmc_diag_canon_claim_cap(unsigned cap) {
+extern "C" KMC_DIAG_API int kmc_diag_canon_claim_cap(unsigned cap) {
     if (cap > (unsigned)kClaimW) return KMC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h_mu);
     h_claim_cap = cap ? cap : kClaimW;
     return KMC_OK;
 }
 
-// Test hook (not in kmc.h): the longest list canon_sort_kernel takes (0: none, so
+// Test hook (diagnostic library only, not in kmc.h): the longest list canon_sort_kernel takes (0: none, so
 // every list goes to canon_table_kernel); any value above kSortCap restores the default.
-extern "C" int kmc_diag_canon_sort_cap(unsigned cap) {
+extern "C" KMC_DIAG_API int kmc_diag_canon_sort_cap(unsigned cap) {
     std::lock_guard<std::mutex> lk(h_mu);
     h_sort_cap = cap > kSortCap ? kSortCap : cap;
     return KMC_OK;
 }
+#endif
 
-
-extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k,
-                                        unsigned flags, uint64_t *keys, uint32_t *counts, uint64_t capacity,
-                                        uint64_t *rec_offsets, uint64_t *num_distinct, hipStream_t stream) {
-    if (k < 1 || k > KMC_CANON_MAX_K) return KMC_ERR_UNSUPPORTED_K;
-    if (!num_distinct) return KMC_ERR_INVALID_ARG;
-    *num_distinct = 0;
-    if (num_seqs == 0) return KMC_OK;
-    if (!data || !indices || !rec_offsets) return KMC_ERR_INVALID_ARG;
-    if (reinterpret_cast<uintptr_t>(data) & 15u) return KMC_ERR_ALIGNMENT;
-    const int64_t n = (int64_t)num_seqs;
-    std::vector<int64_t> hidx(n + 1);
-    hipError_t he = hipMemcpyAsync(hidx.data(), indices, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(stream);
-    if (he != hipSuccess) return (int)he;
-    for (int64_t r = 0; r < n; ++r)
-        if (hidx[r + 1] < hidx[r]) return KMC_ERR_INVALID_ARG;
-    int device = 0, cus = 0;
-    if ((he = hipGetDevice(&device)) || (he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)))
-        return (int)he;
-    // geometry of K1 / K3a: G workgroups over the window chunks
-    HParams p{};
-    p.data = data;
-    p.idx = indices;
-    p.n = n;
-    p.lo = hidx[0];
-    p.hi = hidx[n];
-    p.k = k;
-    p.flags = flags;
-    p.c_lo = p.lo >> 4;
-    const int64_t chunks = p.hi > p.lo ? ((p.hi + 15) >> 4) - p.c_lo : 0;
-    p.G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, chunks));
-    p.cpw = std::max<int64_t>(1, (chunks + p.G - 1) / p.G);
-    // per record: lists, coarse buckets, workgroups holding its windows, cnt
-    // layouts, list ids, K3b workgroups
-    std::vector<uint8_t> lg(n);
-    std::vector<int32_t> w0(n), nwg(n);
-    std::vector<int64_t> cbase(n + 1), ccbase(n + 1), lbase(n + 1);
+namespace {
+// Geometry and workspace layout of one canonical call, from the host copy of the
+// (biased) record offsets: K1 / K3a chunk split, per-record lists / coarse
+// buckets / workgroups, cnt layouts, list ids, K3b workgroups.
+struct CanonPlan {
+    int64_t c_lo = 0, cpw = 1;
+    int G = 1;
+    std::vector<uint8_t> lg;
+    std::vector<int32_t> w0, nwg;
+    std::vector<int64_t> cbase, ccbase, lbase;
     std::vector<int2> fsplit;
+    int64_t M = 0, Mc = 0, L = 0, windows = 0;
+    size_t o_idx, o_lg, o_cb, o_ccb, o_w0, o_nw, o_lb, o_fs, o_cnt, o_off, o_cntc, o_offc, o_bs, o_ent, o_ls, o_pk,
+        o_pc, o_nd, o_do, o_err, o_dn, o_dl, total;
+};
+
+void canon_plan(const int64_t *hidx, int64_t n, int k, int cus, CanonPlan &P) {
+    const int64_t lo = hidx[0], hi = hidx[n];
+    P.c_lo = lo >> 4;
+    const int64_t chunks = hi > lo ? ((hi + 15) >> 4) - P.c_lo : 0;
+    P.G = (int)std::max<int64_t>(1, std::min<int64_t>(cus, chunks));
+    P.cpw = std::max<int64_t>(1, (chunks + P.G - 1) / P.G);
+    P.lg.assign(n, 0);
+    P.w0.assign(n, 0);
+    P.nwg.assign(n, 0);
+    P.cbase.assign(n + 1, 0);
+    P.ccbase.assign(n + 1, 0);
+    P.lbase.assign(n + 1, 0);
+    P.fsplit.clear();
     int64_t M = 0, Mc = 0, L = 0, windows = 0;
     for (int64_t r = 0; r < n; ++r) {
         const int64_t a = hidx[r], nw = std::max<int64_t>(0, hidx[r + 1] - a - k);
@@ -1234,56 +1227,146 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
         int g = 0;
         while (g < kMaxLg && ((int64_t)kListTarget << g) < nw) ++g;
         const int gc = g < kCoarseLg ? g : kCoarseLg;
-        lg[r] = (uint8_t)g;
+        P.lg[r] = (uint8_t)g;
         if (nw > 0) {
             const int64_t cf = a >> 4, cl = (a + nw - 1) >> 4;
-            w0[r] = (int32_t)((cf - p.c_lo) / p.cpw);
-            nwg[r] = (int32_t)((cl - p.c_lo) / p.cpw) - w0[r] + 1;
-        } else {
-            w0[r] = 0;
-            nwg[r] = 0;
+            P.w0[r] = (int32_t)((cf - P.c_lo) / P.cpw);
+            P.nwg[r] = (int32_t)((cl - P.c_lo) / P.cpw) - P.w0[r] + 1;
         }
-        cbase[r] = M;
-        ccbase[r] = Mc;
-        lbase[r] = L;
-        M += ((int64_t)1 << g) * nwg[r];
-        Mc += ((int64_t)1 << gc) * nwg[r];
+        P.cbase[r] = M;
+        P.ccbase[r] = Mc;
+        P.lbase[r] = L;
+        M += ((int64_t)1 << g) * P.nwg[r];
+        Mc += ((int64_t)1 << gc) * P.nwg[r];
         L += (int64_t)1 << g;
         if (g > gc && nw > 0)
-            for (int c = 0; c < (1 << gc); ++c) fsplit.push_back(make_int2((int)r, c));
+            for (int c = 0; c < (1 << gc); ++c) P.fsplit.push_back(make_int2((int)r, c));
     }
-    cbase[n] = M;
-    ccbase[n] = Mc;
-    lbase[n] = L;
-    p.lists = L;
-    const int64_t NF = (int64_t)fsplit.size();
+    P.cbase[n] = M;
+    P.ccbase[n] = Mc;
+    P.lbase[n] = L;
+    P.M = M;
+    P.Mc = Mc;
+    P.L = L;
+    P.windows = windows;
+    const int64_t NF = (int64_t)P.fsplit.size();
     const int64_t cap_w = std::max<int64_t>(windows, 1);
-    // workspace
     size_t o = 0;
-    const size_t o_lg = o; o += al256(n);
-    const size_t o_cb = o; o += al256((n + 1) * 8);
-    const size_t o_ccb = o; o += al256((n + 1) * 8);
-    const size_t o_w0 = o; o += al256(n * 4);
-    const size_t o_nw = o; o += al256(n * 4);
-    const size_t o_lb = o; o += al256((n + 1) * 8);
-    const size_t o_fs = o; o += al256((size_t)std::max<int64_t>(NF, 1) * sizeof(int2));
-    const size_t o_cnt = o; o += al256((size_t)std::max<int64_t>(M, 1) * 4);
-    const size_t o_off = o; o += al256((size_t)(M + 1) * 8);
-    const size_t o_cntc = o; o += al256((size_t)std::max<int64_t>(Mc, 1) * 4);
-    const size_t o_offc = o; o += al256((size_t)(Mc + 1) * 8);
-    const size_t o_bs = o; o += al256((size_t)(scan_tiles(std::max<int64_t>(M, L)) + 1) * 8);
-    const size_t o_ent = o; o += al256((size_t)cap_w * 8);
-    const size_t o_ls = o; o += al256((size_t)(L + 1) * 8);
-    const size_t o_pk = o; o += al256((size_t)cap_w * 8);
-    const size_t o_pc = o; o += al256((size_t)cap_w * 4);
-    const size_t o_nd = o; o += al256((size_t)L * 4);
-    const size_t o_do = o; o += al256((size_t)(L + 1) * 8);
-    const size_t o_err = o; o += al256(4);
-    const size_t o_dn = o; o += al256(8);
-    const size_t o_dl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
-    const size_t total = o;
+    P.o_idx = o; o += al256((n + 1) * 8);
+    P.o_lg = o; o += al256(n);
+    P.o_cb = o; o += al256((n + 1) * 8);
+    P.o_ccb = o; o += al256((n + 1) * 8);
+    P.o_w0 = o; o += al256(n * 4);
+    P.o_nw = o; o += al256(n * 4);
+    P.o_lb = o; o += al256((n + 1) * 8);
+    P.o_fs = o; o += al256((size_t)std::max<int64_t>(NF, 1) * sizeof(int2));
+    P.o_cnt = o; o += al256((size_t)std::max<int64_t>(M, 1) * 4);
+    P.o_off = o; o += al256((size_t)(M + 1) * 8);
+    P.o_cntc = o; o += al256((size_t)std::max<int64_t>(Mc, 1) * 4);
+    P.o_offc = o; o += al256((size_t)(Mc + 1) * 8);
+    P.o_bs = o; o += al256((size_t)(scan_tiles(std::max<int64_t>(M, L)) + 1) * 8);
+    P.o_ent = o; o += al256((size_t)cap_w * 8);
+    P.o_ls = o; o += al256((size_t)(L + 1) * 8);
+    P.o_pk = o; o += al256((size_t)cap_w * 8);
+    P.o_pc = o; o += al256((size_t)cap_w * 4);
+    P.o_nd = o; o += al256((size_t)L * 4);
+    P.o_do = o; o += al256((size_t)(L + 1) * 8);
+    P.o_err = o; o += al256(4);
+    P.o_dn = o; o += al256(8);
+    P.o_dl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
+    P.total = o;
+}
+
+int device_cus(int device, int *cus) {
+    hipError_t he = hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, device);
+    return he == hipSuccess ? 0 : (int)he;
+}
+}  // namespace
+
+extern "C" size_t kmc_count_canonical_workspace_size(const int64_t *host_indices, uint64_t num_seqs, int k,
+                                                    int device) {
+    if (!host_indices || k < 1 || k > KMC_CANON_MAX_K || num_seqs == 0) return 0;
+    int cus = 0;
+    if (device_cus(device, &cus)) return 0;
+    const int64_t n = (int64_t)num_seqs;
+    for (int64_t r = 0; r < n; ++r)
+        if (host_indices[r + 1] < host_indices[r]) return 0;
+    // the size for every alignment of `data` (a misaligned pointer shifts the offsets
+    // by up to 15 bytes, which can move a record's chunks to another workgroup)
+    std::vector<int64_t> b(n + 1);
+    size_t best = 0;
+    CanonPlan P;
+    for (int mis = 0; mis < 16; ++mis) {
+        for (int64_t r = 0; r <= n; ++r) b[r] = host_indices[r] + mis;
+        canon_plan(b.data(), n, k, cus, P);
+        best = std::max(best, P.total);
+    }
+    return best;
+}
+
+extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k,
+                                        unsigned flags, uint64_t *keys, uint32_t *counts, uint64_t capacity,
+                                        uint64_t *rec_offsets, uint64_t *num_distinct, hipStream_t stream) {
+    return kmc_count_canonical_hash_ex(data, indices, num_seqs, k, flags, keys, counts, capacity, rec_offsets,
+                                       num_distinct, nullptr, 0, stream);
+}
+
+extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indices, uint64_t num_seqs, int k,
+                                           unsigned flags, uint64_t *keys, uint32_t *counts, uint64_t capacity,
+                                           uint64_t *rec_offsets, uint64_t *num_distinct, void *workspace,
+                                           size_t workspace_bytes, hipStream_t stream) {
+    if (k < 1 || k > KMC_CANON_MAX_K) return KMC_ERR_UNSUPPORTED_K;
+    if (!num_distinct) return KMC_ERR_INVALID_ARG;
+    *num_distinct = 0;
+    if (num_seqs == 0) return KMC_OK;
+    if (!data || !indices || !rec_offsets) return KMC_ERR_INVALID_ARG;
+    const int64_t n = (int64_t)num_seqs;
+    std::vector<int64_t> hidx(n + 1);
+    hipError_t he = hipMemcpyAsync(hidx.data(), indices, (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(stream);
+    if (he != hipSuccess) return (int)he;
+    for (int64_t r = 0; r < n; ++r)
+        if (hidx[r + 1] < hidx[r]) return KMC_ERR_INVALID_ARG;
+    // any `data` pointer: rounded down to 16 bytes, every offset moved up by the
+    // difference (the kernels read whole 16-byte chunks of the aligned buffer; the
+    // rounded-down bytes share data's page and lie outside every record)
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(data) & 15u;
+    for (auto &x : hidx) x += (int64_t)mis;
+    int device = 0, cus = 0;
+    if ((he = hipGetDevice(&device))) return (int)he;
+    if (int e = device_cus(device, &cus)) return e;
+    CanonPlan P;
+    canon_plan(hidx.data(), n, k, cus, P);
+    HParams p{};
+    p.data = data - mis;
+    p.n = n;
+    p.lo = hidx[0];
+    p.hi = hidx[n];
+    p.k = k;
+    p.flags = flags;
+    p.c_lo = P.c_lo;
+    p.G = P.G;
+    p.cpw = P.cpw;
+    const int64_t M = P.M, Mc = P.Mc, L = P.L;
+    p.lists = L;
+    const int64_t NF = (int64_t)P.fsplit.size();
+    const size_t total = P.total;
+    const size_t o_idx = P.o_idx, o_lg = P.o_lg, o_cb = P.o_cb, o_ccb = P.o_ccb, o_w0 = P.o_w0, o_nw = P.o_nw,
+                 o_lb = P.o_lb, o_fs = P.o_fs, o_cnt = P.o_cnt, o_off = P.o_off, o_cntc = P.o_cntc,
+                 o_offc = P.o_offc, o_bs = P.o_bs, o_ent = P.o_ent, o_ls = P.o_ls, o_pk = P.o_pk, o_pc = P.o_pc,
+                 o_nd = P.o_nd, o_do = P.o_do, o_err = P.o_err, o_dn = P.o_dn, o_dl = P.o_dl;
+    const auto &lg = P.lg;
+    const auto &w0 = P.w0;
+    const auto &nwg = P.nwg;
+    const auto &cbase = P.cbase;
+    const auto &ccbase = P.ccbase;
+    const auto &lbase = P.lbase;
+    const auto &fsplit = P.fsplit;
     char *ws;
-    {
+    if (workspace) {
+        if (workspace_bytes < total) return KMC_ERR_WORKSPACE;
+        ws = static_cast<char *>(workspace);
+    } else {
         std::lock_guard<std::mutex> lk(h_mu);
         if ((int)h_ws.size() <= device) h_ws.resize(device + 1);
         HCache &c = h_ws[device];
@@ -1296,6 +1379,7 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
         }
         ws = static_cast<char *>(c.ptr);
     }
+    p.idx = reinterpret_cast<int64_t *>(ws + o_idx);
     p.lg = reinterpret_cast<uint8_t *>(ws + o_lg);
     p.cbase = reinterpret_cast<int64_t *>(ws + o_cb);
     p.ccbase = reinterpret_cast<int64_t *>(ws + o_ccb);
@@ -1323,7 +1407,8 @@ extern "C" int kmc_count_canonical_hash(const char *data, const int64_t *indices
     p.rec_off = rec_offsets;
     p.out_keys = keys;
     p.out_counts = counts;
-    if ((he = hipMemcpyAsync((void *)p.lg, lg.data(), n, hipMemcpyHostToDevice, stream)) ||
+    if ((he = hipMemcpyAsync((void *)p.idx, hidx.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
+        (he = hipMemcpyAsync((void *)p.lg, lg.data(), n, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.cbase, cbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.ccbase, ccbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.w0, w0.data(), n * 4, hipMemcpyHostToDevice, stream)) ||

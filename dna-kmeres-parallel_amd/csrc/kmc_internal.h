@@ -5,6 +5,11 @@
 struct kmc_dense_args;
 typedef struct ihipStream_t *hipStream_t;
 
+// Test hooks (kmc_diag_*) exist only in the diagnostic library lib/libkmc_diag.so
+// (built with -DKMC_DIAG_HOOKS for the tests that force an algorithm choice);
+// libkmc.so exports exactly the entry points of kmc.h.
+#define KMC_DIAG_API __attribute__((visibility("default")))
+
 namespace kmc {
 typedef struct ihipEvent_t *hipEvent_t;
 // Grid extents of the per-record / per-list helper kernels, which loop over the

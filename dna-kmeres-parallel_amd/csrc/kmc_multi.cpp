@@ -48,99 +48,140 @@ extern "C" int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k,
 
 namespace {
 
-// Communicators of one device set, created on first use (ncclCommInitAll is a
-// collective setup of its own, far dearer than a 21 MB all-reduce) and kept until
-// kmc_multi_release().  RCCL communicators are not thread-safe, so every entry
-// carries its own mutex, held by a kmc_count_multi call from ncclGroupStart until
-// its copy-back has synchronised: calls on the same device set serialise their
-// collectives, calls on disjoint sets run concurrently.  An entry whose collective
-// failed is dropped (and its communicators aborted), so the next call on that set
-// builds fresh ones instead of reusing a communicator in an error state.
-struct CommSet {
+// Per-device state of kmc_count_multi, created on a device's first call and kept
+// until kmc_multi_release(): the stream, two pinned staging buffers, and grow-only
+// device buffers (shard + halo, offsets, count matrix, invalid vector, workspace),
+// so a second call on the same device set allocates nothing (one-shot CLI use
+// paid ~10 hipMalloc/hipHostMalloc per device and call before).  Each device has a
+// mutex that a call holds from its first allocation to its copy-back; a call
+// takes the mutexes of its devices in ascending device order, so calls on
+// overlapping sets ({0,1} and {1,2}) serialise instead of running RCCL
+// collectives concurrently on communicators that share a GPU, and cannot
+// deadlock; calls on disjoint sets run concurrently.
+struct DevState {
     std::mutex mu;
-    std::vector<ncclComm_t> comms;
+    int dev = 0;
+    hipStream_t st = nullptr;
+    char *pin[2] = {nullptr, nullptr};  // pinned staging of the host -> device copy
+    hipEvent_t done[2] = {nullptr, nullptr};
+    char *data = nullptr;
+    size_t data_cap = 0;
+    int64_t *idx = nullptr;
+    size_t idx_cap = 0;
+    int32_t *sum = nullptr;
+    size_t sum_cap = 0;
+    int32_t *inv = nullptr;
+    size_t inv_cap = 0;
+    void *ws = nullptr;
+    size_t ws_cap = 0;
+    int rc = KMC_OK;  // result of this call's load + count (written by its worker thread)
 };
-std::mutex g_comm_mu;
-std::map<std::vector<int>, std::shared_ptr<CommSet>> g_comms;
 
-int comms_for(const std::vector<int> &devs, std::shared_ptr<CommSet> &out) {
-    std::lock_guard<std::mutex> lk(g_comm_mu);
+std::mutex g_mu;                                       // guards the two maps below
+std::map<int, std::unique_ptr<DevState>> g_dev;        // device -> state (stable addresses)
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;  // sorted device set -> comms
+
+DevState *dev_state(int dev) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto &p = g_dev[dev];
+    if (!p) {
+        p.reset(new DevState);
+        p->dev = dev;
+    }
+    return p.get();
+}
+
+void free_state(DevState &d) {  // caller holds d.mu
+    (void)hipSetDevice(d.dev);
+    if (d.st) (void)hipStreamSynchronize(d.st);
+    (void)hipFree(d.data);
+    (void)hipFree(d.idx);
+    (void)hipFree(d.sum);
+    (void)hipFree(d.inv);
+    (void)hipFree(d.ws);
+    for (int j = 0; j < 2; ++j) {
+        if (d.pin[j]) (void)hipHostFree(d.pin[j]);
+        if (d.done[j]) (void)hipEventDestroy(d.done[j]);
+        d.pin[j] = nullptr;
+        d.done[j] = nullptr;
+    }
+    if (d.st) (void)hipStreamDestroy(d.st);
+    d.st = nullptr;
+    d.data = nullptr;
+    d.idx = nullptr;
+    d.sum = nullptr;
+    d.inv = nullptr;
+    d.ws = nullptr;
+    d.data_cap = d.idx_cap = d.sum_cap = d.inv_cap = d.ws_cap = 0;
+}
+
+// Grow a cached device buffer to at least `bytes` (contents are not kept).
+template <class T>
+bool reserve(T *&p, size_t &cap, size_t bytes) {
+    if (bytes <= cap && p) return true;
+    (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&p), bytes ? bytes : 16) != hipSuccess) return false;
+    cap = bytes;
+    return true;
+}
+
+// The communicators of a sorted device set, created on first use (ncclCommInitAll
+// is a collective setup of its own, far dearer than a 21 MB all-reduce).  The caller
+// holds every device mutex of the set, so no other call uses these communicators.
+int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
+    std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_comms.find(devs);
     if (it == g_comms.end()) {
-        auto cs = std::make_shared<CommSet>();
-        cs->comms.resize(devs.size());
-        if (ncclCommInitAll(cs->comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) return KMC_ERR_RCCL;
-        it = g_comms.emplace(devs, std::move(cs)).first;
+        std::vector<ncclComm_t> c(devs.size());
+        if (ncclCommInitAll(c.data(), (int)devs.size(), devs.data()) != ncclSuccess) return KMC_ERR_RCCL;
+        it = g_comms.emplace(devs, std::move(c)).first;
     }
     out = it->second;
     return KMC_OK;
 }
 
-// Remove a failed set from the cache (if it is still the cached one) and abort its
-// communicators.  The caller holds cs->mu.
-void drop_comms(const std::vector<int> &devs, const std::shared_ptr<CommSet> &cs) {
+// A set whose collective failed is dropped and its communicators aborted, so the
+// next call builds fresh ones instead of reusing a communicator in an error state.
+void drop_comms(const std::vector<int> &devs) {
+    std::vector<ncclComm_t> c;
     {
-        std::lock_guard<std::mutex> lk(g_comm_mu);
+        std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_comms.find(devs);
-        if (it != g_comms.end() && it->second == cs) g_comms.erase(it);
+        if (it == g_comms.end()) return;
+        c.swap(it->second);
+        g_comms.erase(it);
     }
-    for (auto &c : cs->comms) (void)ncclCommAbort(c);
-    cs->comms.clear();
-}
-
-struct DevBufs {
-    int dev = 0;
-    hipStream_t st = nullptr;
-    char *data = nullptr;
-    int64_t *idx = nullptr;
-    int32_t *sum = nullptr;
-    int32_t *inv = nullptr;
-    void *ws = nullptr;
-    char *pin[2] = {nullptr, nullptr};  // pinned staging of the host -> device copy
-    hipEvent_t done[2] = {nullptr, nullptr};
-    int rc = KMC_OK;
-};
-
-void release(std::vector<DevBufs> &b) {
-    for (auto &d : b) {
-        (void)hipSetDevice(d.dev);
-        if (d.st) (void)hipStreamSynchronize(d.st);
-        (void)hipFree(d.data);
-        (void)hipFree(d.idx);
-        (void)hipFree(d.sum);
-        (void)hipFree(d.inv);
-        (void)hipFree(d.ws);
-        for (int j = 0; j < 2; ++j) {
-            if (d.pin[j]) (void)hipHostFree(d.pin[j]);
-            if (d.done[j]) (void)hipEventDestroy(d.done[j]);
-        }
-        if (d.st) (void)hipStreamDestroy(d.st);
-    }
+    for (auto &x : c) (void)ncclCommAbort(x);
 }
 
 constexpr size_t kStage = (size_t)32 << 20;  // bytes per pinned staging buffer
 
-// Host thread of one device: allocate, stream the shard + halo through two pinned
-// buffers (the host copy into one overlaps the DMA out of the other), count.  One
-// thread per device, so every device loads at the same time.
-void load_and_count(DevBufs &d, const char *data, const int64_t *indices, uint64_t num_seqs, int k,
+// Host thread of one device: (re)use its buffers, stream the shard + halo through
+// two pinned buffers (the host copy into one overlaps the DMA out of the other),
+// count.  One thread per device, so every device loads at the same time.
+void load_and_count(DevState &d, const char *data, const int64_t *indices, uint64_t num_seqs, int k,
                     const kmc_shard &sh, bool want_invalid, size_t sum_bytes) {
     auto bad = [&](int code) { d.rc = code; };
+    d.rc = KMC_OK;
     if (hipSetDevice(d.dev) != hipSuccess) return bad(KMC_ERR_NO_DEVICE);
-    if (hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking) != hipSuccess) return bad(KMC_ERR_NO_DEVICE);
+    if (!d.st && hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking) != hipSuccess) return bad(KMC_ERR_NO_DEVICE);
+    for (int j = 0; j < 2; ++j) {
+        if (!d.pin[j] &&
+            hipHostMalloc(reinterpret_cast<void **>(&d.pin[j]), kStage, hipHostMallocDefault) != hipSuccess)
+            return bad(KMC_ERR_NOMEM);
+        if (!d.done[j] && hipEventCreateWithFlags(&d.done[j], hipEventDisableTiming) != hipSuccess)
+            return bad(KMC_ERR_NOMEM);
+    }
     // the device holds [base, read_hi) with base = read_lo rounded down to 16 so that
     // the library's data pointer (device base - base) stays 16-byte aligned
     const uint64_t base = sh.read_lo & ~(uint64_t)15;
     const uint64_t len = sh.read_hi - base;
-    if (hipMalloc(&d.data, len + 16) != hipSuccess) return bad(KMC_ERR_NOMEM);
-    if (hipMalloc(&d.idx, (num_seqs + 1) * sizeof(int64_t)) != hipSuccess) return bad(KMC_ERR_NOMEM);
-    if (hipMalloc(&d.sum, sum_bytes) != hipSuccess) return bad(KMC_ERR_NOMEM);
-    if (want_invalid && hipMalloc(&d.inv, num_seqs * sizeof(int32_t)) != hipSuccess) return bad(KMC_ERR_NOMEM);
-    for (int j = 0; j < 2; ++j) {
-        if (hipHostMalloc(reinterpret_cast<void **>(&d.pin[j]), kStage, hipHostMallocDefault) != hipSuccess)
-            return bad(KMC_ERR_NOMEM);
-        if (hipEventCreateWithFlags(&d.done[j], hipEventDisableTiming) != hipSuccess) return bad(KMC_ERR_NOMEM);
-    }
+    if (!reserve(d.data, d.data_cap, len + 16)) return bad(KMC_ERR_NOMEM);
+    if (!reserve(d.idx, d.idx_cap, (num_seqs + 1) * sizeof(int64_t))) return bad(KMC_ERR_NOMEM);
+    if (!reserve(d.sum, d.sum_cap, sum_bytes)) return bad(KMC_ERR_NOMEM);
+    if (want_invalid && !reserve(d.inv, d.inv_cap, num_seqs * sizeof(int32_t))) return bad(KMC_ERR_NOMEM);
     kmc_dense_args a{};
     a.data = d.data - base;
     a.indices = d.idx;
@@ -148,17 +189,18 @@ void load_and_count(DevBufs &d, const char *data, const int64_t *indices, uint64
     a.k = k;
     a.sum = d.sum;
     a.sum_ld = num_seqs;
-    a.invalid = d.inv;
+    a.invalid = want_invalid ? d.inv : nullptr;
     a.read_lo = sh.read_lo;
     a.read_hi = sh.read_hi;
     a.win_lo = sh.win_lo;
     a.win_hi = sh.win_hi;
     const size_t wsb = kmc_count_dense_ex_workspace_size(&a, d.dev);
-    if (wsb == 0 || hipMalloc(&d.ws, wsb) != hipSuccess) return bad(KMC_ERR_NOMEM);
+    if (wsb == 0 || !reserve(d.ws, d.ws_cap, wsb)) return bad(KMC_ERR_NOMEM);
     a.workspace = d.ws;
-    a.workspace_bytes = wsb;
-    // indices are small: one synchronous copy
-    if (hipMemcpy(d.idx, indices, (num_seqs + 1) * sizeof(int64_t), hipMemcpyHostToDevice) != hipSuccess)
+    a.workspace_bytes = d.ws_cap;
+    // indices are small: one copy, ordered before the count on the same stream
+    if (hipMemcpyAsync(d.idx, indices, (num_seqs + 1) * sizeof(int64_t), hipMemcpyHostToDevice, d.st) !=
+        hipSuccess)
         return bad(KMC_ERR_NOMEM);
     uint64_t done = 0;
     for (int j = 0; done < len; j ^= 1) {
@@ -187,9 +229,11 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     for (int i = 0; i < ndev; ++i) {
         devs[i] = devices ? devices[i] : i;
         if (devs[i] < 0 || devs[i] >= visible) return KMC_ERR_INVALID_ARG;
-        for (int j = 0; j < i; ++j)
-            if (devs[j] == devs[i]) return KMC_ERR_INVALID_ARG;  // one communicator rank per device
     }
+    // the set as a sorted list: the communicator cache key and the lock order
+    std::sort(devs.begin(), devs.end());
+    if (std::adjacent_find(devs.begin(), devs.end()) != devs.end())
+        return KMC_ERR_INVALID_ARG;  // one communicator rank per device
     std::vector<kmc_shard> sh(ndev);
     int rc = kmc_plan_shards(indices, num_seqs, k, ndev, 4096, sh.data());
     if (rc) return rc;
@@ -198,77 +242,84 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     int cur = 0;
     (void)hipGetDevice(&cur);
 
-    std::vector<DevBufs> b(ndev);
-    auto fail = [&](int code) {
-        release(b);
-        (void)hipSetDevice(cur);
-        return code;
-    };
+    std::vector<DevState *> b(ndev);
+    std::vector<std::unique_lock<std::mutex>> locks;
+    locks.reserve(ndev);
+    for (int i = 0; i < ndev; ++i) {  // ascending device order: no lock cycles
+        b[i] = dev_state(devs[i]);
+        locks.emplace_back(b[i]->mu);
+    }
     {
         std::vector<std::thread> th;
         th.reserve(ndev);
-        for (int i = 0; i < ndev; ++i) {
-            b[i].dev = devs[i];
-            th.emplace_back(load_and_count, std::ref(b[i]), data, indices, num_seqs, k, std::cref(sh[i]),
+        for (int i = 0; i < ndev; ++i)
+            th.emplace_back(load_and_count, std::ref(*b[i]), data, indices, num_seqs, k, std::cref(sh[i]),
                             invalid != nullptr, sum_bytes);
-        }
         for (auto &t : th) t.join();
     }
-    for (auto &d : b)
-        if (d.rc) return fail(d.rc);
+    for (auto *d : b)
+        if (d->rc) {
+            (void)hipSetDevice(cur);
+            return d->rc;
+        }
     // one all-reduce of the int32 matrix (and the invalid vector) over xGMI
-    std::shared_ptr<CommSet> cs;
-    rc = comms_for(devs, cs);
-    if (rc) return fail(rc);
-    std::unique_lock<std::mutex> use(cs->mu);  // this set's communicators, until the copy-back is done
-    if (cs->comms.empty()) {                   // dropped by a failed call while we waited: build anew
-        use.unlock();
-        cs.reset();
-        rc = comms_for(devs, cs);
-        if (rc) return fail(rc);
-        use = std::unique_lock<std::mutex>(cs->mu);
+    std::vector<ncclComm_t> comms;
+    rc = comms_for(devs, comms);
+    if (rc) {
+        (void)hipSetDevice(cur);
+        return rc;
     }
     ncclResult_t nr = ncclGroupStart();
     for (int i = 0; i < ndev && nr == ncclSuccess; ++i) {
-        nr = ncclAllReduce(b[i].sum, b[i].sum, nb * num_seqs, ncclInt32, ncclSum, cs->comms[i], b[i].st);
+        nr = ncclAllReduce(b[i]->sum, b[i]->sum, nb * num_seqs, ncclInt32, ncclSum, comms[i], b[i]->st);
         if (nr == ncclSuccess && invalid)
-            nr = ncclAllReduce(b[i].inv, b[i].inv, num_seqs, ncclInt32, ncclSum, cs->comms[i], b[i].st);
+            nr = ncclAllReduce(b[i]->inv, b[i]->inv, num_seqs, ncclInt32, ncclSum, comms[i], b[i]->st);
     }
     if (nr == ncclSuccess) nr = ncclGroupEnd();
     else ncclGroupEnd();
     bool comm_ok = nr == ncclSuccess;
     if (comm_ok) {
-        for (auto &d : b) {  // the collective itself finished on every device
-            (void)hipSetDevice(d.dev);
-            if (hipStreamSynchronize(d.st) != hipSuccess) comm_ok = false;
+        for (auto *d : b) {  // the collective itself finished on every device
+            (void)hipSetDevice(d->dev);
+            if (hipStreamSynchronize(d->st) != hipSuccess) comm_ok = false;
         }
         if (!comm_ok) nr = ncclSystemError;
     }
     if (nr == ncclSuccess) {
-        (void)hipSetDevice(b[0].dev);
-        if (hipMemcpyAsync(sum, b[0].sum, sum_bytes, hipMemcpyDeviceToHost, b[0].st) != hipSuccess) nr = ncclSystemError;
-        if (invalid && hipMemcpyAsync(invalid, b[0].inv, num_seqs * sizeof(int32_t), hipMemcpyDeviceToHost,
-                                      b[0].st) != hipSuccess)
+        DevState &d = *b[0];
+        (void)hipSetDevice(d.dev);
+        if (hipMemcpyAsync(sum, d.sum, sum_bytes, hipMemcpyDeviceToHost, d.st) != hipSuccess) nr = ncclSystemError;
+        if (invalid &&
+            hipMemcpyAsync(invalid, d.inv, num_seqs * sizeof(int32_t), hipMemcpyDeviceToHost, d.st) != hipSuccess)
             nr = ncclSystemError;
-        if (hipStreamSynchronize(b[0].st) != hipSuccess) nr = ncclSystemError;
+        if (hipStreamSynchronize(d.st) != hipSuccess) nr = ncclSystemError;
     }
-    if (!comm_ok) drop_comms(devs, cs);
-    use.unlock();
-    release(b);
+    if (!comm_ok) drop_comms(devs);
     (void)hipSetDevice(cur);
-    return nr == ncclSuccess ? KMC_OK : KMC_ERR_RCCL;
+    if (nr != ncclSuccess) return KMC_ERR_RCCL;
+    int st = KMC_OK;  // every device has synchronised: a deferred count overflow is reported now
+    for (auto *d : b)
+        if (kmc_dense_status(d->dev) != KMC_OK) st = KMC_ERR_CAPACITY;
+    return st;
 }
 
 extern "C" int kmc_multi_release(void) {
-    std::map<std::vector<int>, std::shared_ptr<CommSet>> all;
+    // every device mutex, in ascending order, so no call is using a communicator or
+    // a buffer while they are destroyed
+    std::vector<DevState *> all;
     {
-        std::lock_guard<std::mutex> lk(g_comm_mu);
-        all.swap(g_comms);
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (auto &e : g_dev) all.push_back(e.second.get());  // map order = ascending device
     }
-    for (auto &e : all) {
-        std::lock_guard<std::mutex> use(e.second->mu);  // wait for a call still using the set
-        for (auto &c : e.second->comms) ncclCommDestroy(c);
-        e.second->comms.clear();
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (auto *d : all) locks.emplace_back(d->mu);
+    std::map<std::vector<int>, std::vector<ncclComm_t>> comms;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        comms.swap(g_comms);
     }
+    for (auto &e : comms)
+        for (auto &c : e.second) ncclCommDestroy(c);
+    for (auto *d : all) free_state(*d);
     return KMC_OK;
 }

@@ -1178,14 +1178,16 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
 
 }  // namespace
 
-// Test hook (not in kmc.h): see g_radix_mode.
-extern "C" int kmc_diag_radix_mode(int mode, float cap_scale) {
+#ifdef KMC_DIAG_HOOKS
+// Test hook (diagnostic library only, not in kmc.h): see g_radix_mode.
+extern "C" KMC_DIAG_API int kmc_diag_radix_mode(int mode, float cap_scale) {
     if (mode < 0 || mode > 2 || !(cap_scale > 0.0f)) return KMC_ERR_INVALID_ARG;
     std::lock_guard<std::mutex> lk(r_mu);
     g_radix_mode = mode;
     g_cap_scale = cap_scale;
     return KMC_OK;
 }
+#endif
 
 // Entry used by kmc_dense.hip for 9 <= k <= KMC_DENSE_MAX_K.
 int radix_dense(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_only, size_t *size_out) {

@@ -22,6 +22,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("KMC_LIB") or os.path.join(HERE, "lib", "libkmc.so")
+# the diagnostic build (test hooks kmc_diag_*, see diag()); never used by the product path
+DIAG_LIB_PATH = os.environ.get("KMC_DIAG_LIB") or os.path.join(HERE, "lib", "libkmc_diag.so")
 HEADER = os.path.join(REPO, "include", "kmc.h")
 
 DIALECT_BLANK = 0  # importSeqs
@@ -52,59 +54,95 @@ class DenseArgs(ctypes.Structure):
 
 
 _lib = None
+_diag_lib = None
+_active = None  # the diagnostic library while inside diag()
 
 
 def lib():
     """Load libkmc.so (built in-tree by `make -C dna-kmeres-parallel_amd`)."""
     global _lib
+    if _active is not None:
+        return _active
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError("libkmc.so not built: run `make -C %s` (no CPU fallback exists)" % HERE)
-        L = ctypes.CDLL(LIB_PATH)
-        L.kmc_error_string.restype = ctypes.c_char_p
-        L.kmc_error_string.argtypes = [ctypes.c_int]
-        L.kmc_version.restype = ctypes.c_int
-        L.sumKmereCoincidencesGlobalMemory_hip.argtypes = [_P, _P, ctypes.c_uint, _P, _P]
-        L.kmc_count_dense_workspace_size.restype = ctypes.c_size_t
-        L.kmc_count_dense_workspace_size.argtypes = [ctypes.c_int, _U64, _U64, ctypes.c_int]
-        L.kmc_count_dense.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, _P, _P, _P, ctypes.c_size_t, _P]
-        L.kmc_count_dense_ex.argtypes = [ctypes.POINTER(DenseArgs), _P]
-        L.kmc_count_dense_ex_workspace_size.restype = ctypes.c_size_t
-        L.kmc_count_dense_ex_workspace_size.argtypes = [ctypes.POINTER(DenseArgs), ctypes.c_int]
-        L.kmc_trace_set_events.argtypes = [_P, _P]
-        if hasattr(L, "kmc_set_reserved_cus"):  # (absent from builds before round 3)
-            L.kmc_set_reserved_cus.argtypes = [ctypes.c_int]
-        L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
-        L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
-        L.kmc_multi_release.argtypes = []
-        L.kmc_synth_fill.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
-        L.kmc_synth_fill_range.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
-        L.kmc_synth_indices.argtypes = [_P, _U64, _U64]
-        L.kmc_synth_indices.restype = None
-        L.kmc_fasta_load.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P)]
-        for fn in ("kmc_fasta_num_seqs", "kmc_fasta_data_bytes", "kmc_fasta_reference_num_indexes"):
-            getattr(L, fn).restype = _U64
-            getattr(L, fn).argtypes = [_P]
-        L.kmc_fasta_indices.restype = _P
-        L.kmc_fasta_indices.argtypes = [_P]
-        L.kmc_fasta_data.restype = _P
-        L.kmc_fasta_data.argtypes = [_P]
-        L.kmc_fasta_free.argtypes = [_P]
-        L.kmc_fasta_free.restype = None
-        L.kmc_fasta_parse_device.argtypes = [_P, _U64, ctypes.c_int, _P, _U64, _P, _U64, ctypes.POINTER(_U64),
-                                             ctypes.POINTER(_U64), _P]
-        L.kmc_fasta_load_device.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P),
-                                            ctypes.POINTER(_U64), ctypes.POINTER(_P), ctypes.POINTER(_U64), _P]
-        L.kmc_pair_distances_workspace_size.restype = ctypes.c_size_t
-        L.kmc_pair_distances_workspace_size.argtypes = [_U64, ctypes.c_int, ctypes.c_int]
-        L.kmc_pair_distances.argtypes = [_P, _U64, _P, _U64, ctypes.c_int, _P, _P, ctypes.c_size_t, _P]
-        L.minKmeres2_hip.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P, _P]
-        if hasattr(L, "kmc_diag_radix_mode"):  # test hook (not in kmc.h; absent from older builds)
-            L.kmc_diag_radix_mode.argtypes = [ctypes.c_int, ctypes.c_float]
-        L.kmc_count_canonical_hash.argtypes = [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _P, _P, _U64, _P,
-                                               ctypes.POINTER(_U64), _P]
-        _lib = L
+        _lib = _load(LIB_PATH)
     return _lib
+
+
+class diag:
+    """Context manager: inside it every binding calls lib/libkmc_diag.so, the same
+    library built with the test hooks (kmc_diag_radix_mode, kmc_diag_canon_claim_cap,
+    kmc_diag_canon_sort_cap, kmc_diag_dense_spill_cap) that force an algorithm
+    choice; libkmc.so exports none of them.  `with kmc.diag() as D: D.kmc_diag_...`"""
+
+    def __enter__(self):
+        global _diag_lib, _active
+        if _diag_lib is None:
+            _diag_lib = _load(DIAG_LIB_PATH)
+            _diag_lib.kmc_diag_radix_mode.argtypes = [ctypes.c_int, ctypes.c_float]
+            _diag_lib.kmc_diag_canon_claim_cap.argtypes = [ctypes.c_uint]
+            _diag_lib.kmc_diag_canon_sort_cap.argtypes = [ctypes.c_uint]
+            _diag_lib.kmc_diag_dense_spill_cap.argtypes = [ctypes.c_uint]
+        self._prev = _active
+        _active = _diag_lib
+        return _diag_lib
+
+    def __exit__(self, *exc):
+        global _active
+        L = _active
+        # restore the defaults for the next user of the diagnostic library
+        L.kmc_diag_radix_mode(0, 1.0)
+        L.kmc_diag_canon_claim_cap(0)
+        L.kmc_diag_canon_sort_cap(1 << 30)
+        L.kmc_diag_dense_spill_cap(0)
+        _active = self._prev
+        return False
+
+
+def _load(path):
+    if not os.path.exists(path):
+        raise RuntimeError("%s not built: run `make -C %s` (no CPU fallback exists)" % (os.path.basename(path), HERE))
+    L = ctypes.CDLL(path)
+    L.kmc_error_string.restype = ctypes.c_char_p
+    L.kmc_error_string.argtypes = [ctypes.c_int]
+    L.kmc_version.restype = ctypes.c_int
+    L.sumKmereCoincidencesGlobalMemory_hip.argtypes = [_P, _P, ctypes.c_uint, _P, _P]
+    L.kmc_count_dense_workspace_size.restype = ctypes.c_size_t
+    L.kmc_count_dense_workspace_size.argtypes = [ctypes.c_int, _U64, _U64, ctypes.c_int]
+    L.kmc_count_dense.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, _P, _P, _P, ctypes.c_size_t, _P]
+    L.kmc_count_dense_ex.argtypes = [ctypes.POINTER(DenseArgs), _P]
+    L.kmc_count_dense_ex_workspace_size.restype = ctypes.c_size_t
+    L.kmc_count_dense_ex_workspace_size.argtypes = [ctypes.POINTER(DenseArgs), ctypes.c_int]
+    L.kmc_dense_status.argtypes = [ctypes.c_int]
+    L.kmc_trace_set_events.argtypes = [_P, _P]
+    L.kmc_set_reserved_cus.argtypes = [ctypes.c_int]
+    L.kmc_plan_shards.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int, _U64, _P]
+    L.kmc_count_multi.argtypes = [_P, _P, _U64, _U64, ctypes.c_int, ctypes.c_int, _P, _P, _P]
+    L.kmc_multi_release.argtypes = []
+    L.kmc_synth_fill.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
+    L.kmc_synth_fill_range.argtypes = [_P, _U64, _U64, _U64, _U64, _P]
+    L.kmc_synth_indices.argtypes = [_P, _U64, _U64]
+    L.kmc_synth_indices.restype = None
+    L.kmc_fasta_load.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P)]
+    for fn in ("kmc_fasta_num_seqs", "kmc_fasta_data_bytes", "kmc_fasta_reference_num_indexes"):
+        getattr(L, fn).restype = _U64
+        getattr(L, fn).argtypes = [_P]
+    L.kmc_fasta_indices.restype = _P
+    L.kmc_fasta_indices.argtypes = [_P]
+    L.kmc_fasta_data.restype = _P
+    L.kmc_fasta_data.argtypes = [_P]
+    L.kmc_fasta_free.argtypes = [_P]
+    L.kmc_fasta_free.restype = None
+    L.kmc_fasta_parse_device.argtypes = [_P, _U64, ctypes.c_int, _P, _U64, _P, _U64, ctypes.POINTER(_U64),
+                                         ctypes.POINTER(_U64), _P]
+    L.kmc_fasta_load_device.argtypes = [ctypes.c_char_p, ctypes.c_int, _I64, ctypes.POINTER(_P),
+                                        ctypes.POINTER(_U64), ctypes.POINTER(_P), ctypes.POINTER(_U64), _P]
+    L.kmc_pair_distances_workspace_size.restype = ctypes.c_size_t
+    L.kmc_pair_distances_workspace_size.argtypes = [_U64, ctypes.c_int, ctypes.c_int]
+    L.kmc_pair_distances.argtypes = [_P, _U64, _P, _U64, ctypes.c_int, _P, _P, ctypes.c_size_t, _P]
+    L.minKmeres2_hip.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P, _P]
+    L.kmc_count_canonical_hash.argtypes = [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _P, _P, _U64, _P,
+                                           ctypes.POINTER(_U64), _P]
+    return L
 
 
 def error_string(code):
@@ -229,10 +267,12 @@ CANON_FORWARD = 2
 CANON_MAX_K = 31
 
 
-def count_canonical(data, indices, k, flags=0, capacity=None, stream=None):
-    """Canonical k-mer counts per record (kmc_count_canonical_hash): returns
+def count_canonical(data, indices, k, flags=0, capacity=None, workspace=None, stream=None):
+    """Canonical k-mer counts per record (kmc_count_canonical_hash[_ex]): returns
     (keys uint64 as int64 tensor, counts int32 tensor, rec_offsets int64 tensor);
-    record s owns [rec_offsets[s], rec_offsets[s+1]), order within it unspecified."""
+    record s owns [rec_offsets[s], rec_offsets[s+1]), order within it unspecified.
+    `workspace`: a caller device buffer of canonical_workspace_size() bytes (None:
+    the library's own)."""
     import torch
     n = indices.numel() - 1
     if capacity is None:
@@ -241,11 +281,23 @@ def count_canonical(data, indices, k, flags=0, capacity=None, stream=None):
     counts = torch.empty(capacity, dtype=torch.int32, device=data.device)
     off = torch.zeros(max(n + 1, 1), dtype=torch.int64, device=data.device)
     tot = _U64(0)
-    rc = lib().kmc_count_canonical_hash(_dptr(data), _dptr(indices), n, k, flags, _dptr(keys), _dptr(counts),
-                                        capacity, _dptr(off), ctypes.byref(tot), _stream(stream))
+    if workspace is None:
+        rc = lib().kmc_count_canonical_hash(_dptr(data), _dptr(indices), n, k, flags, _dptr(keys), _dptr(counts),
+                                            capacity, _dptr(off), ctypes.byref(tot), _stream(stream))
+    else:
+        rc = lib().kmc_count_canonical_hash_ex(_dptr(data), _dptr(indices), n, k, flags, _dptr(keys),
+                                               _dptr(counts), capacity, _dptr(off), ctypes.byref(tot),
+                                               _dptr(workspace), workspace.numel() * workspace.element_size(),
+                                               _stream(stream))
     _check(rc, "kmc_count_canonical_hash")
     t = int(tot.value)
     return keys[:t], counts[:t], off
+
+
+def canonical_workspace_size(indices_host, k, device=0):
+    """kmc_count_canonical_workspace_size for host int64 offsets (num_seqs + 1)."""
+    idx = np.ascontiguousarray(indices_host, dtype=np.int64)
+    return int(lib().kmc_count_canonical_workspace_size(idx.ctypes.data_as(_P), idx.size - 1, k, device))
 
 
 def min_kmeres2(sums, mins, num_seqs, current_seq, indexes, stream=None):

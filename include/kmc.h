@@ -30,6 +30,14 @@
 extern "C" {
 #endif
 
+/* libkmc.so is built with hidden visibility: exactly the entry points declared
+ * here are exported (tests/test_abi.py compares `nm -D` with this header). */
+#if defined(__GNUC__) || defined(__clang__)
+#define KMC_API __attribute__((visibility("default")))
+#else
+#define KMC_API
+#endif
+
 #ifndef KMC_HIP_STREAM_T_DEFINED
 #define KMC_HIP_STREAM_T_DEFINED
 typedef struct ihipStream_t *hipStream_t; /* identical to HIP's own typedef */
@@ -60,10 +68,10 @@ enum kmc_status {
 };
 
 /* Human-readable text for a kmc_status or hipError_t code (static storage). */
-const char *kmc_error_string(int code);
+KMC_API const char *kmc_error_string(int code);
 
 /* Library version: major*10000 + minor*100 + patch. */
-int kmc_version(void);
+KMC_API int kmc_version(void);
 
 /* ------------------------------------------------------------------------ */
 /* Exact drop-in for the reference launch
@@ -81,7 +89,7 @@ int kmc_version(void);
  * counted).  Uses a library-owned device workspace (allocated on first use per device).
  * Asynchronous on `stream` (0 = the null stream); the reference synchronises
  * after the launch (main.cu:291), so should the caller. */
-int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_seqs, int *sum,
+KMC_API int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_seqs, int *sum,
                                          hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
@@ -98,9 +106,9 @@ int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsigned num_
  *               overlap (one stream, or the caller serialises them), and they are
  *               not graph-capture safe.  Concurrent calls pass their own workspace.
  * The same holds for the NULL workspace of kmc_pair_distances.  */
-size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device);
+KMC_API size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device);
 
-int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,
+KMC_API int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,
                     int k, int32_t *sum, int32_t *invalid, void *workspace, size_t workspace_bytes,
                     hipStream_t stream);
 
@@ -123,8 +131,19 @@ typedef struct kmc_dense_args {
     size_t workspace_bytes;
 } kmc_dense_args;
 
-size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *args, int device);
-int kmc_count_dense_ex(const kmc_dense_args *args, hipStream_t stream);
+KMC_API size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *args, int device);
+KMC_API int kmc_count_dense_ex(const kmc_dense_args *args, hipStream_t stream);
+
+/* Deferred device-side status of the asynchronous dense calls on `device`.  The
+ * k = 8 kernel keeps its 16-bit counters exact with spill entries whose number per
+ * workgroup is bounded analytically (one per >= 4096 windows); should a workgroup
+ * ever emit more than its workspace holds, the kernel raises a flag in host-mapped
+ * memory instead of returning short counts silently.  This call (after the stream
+ * has synchronised) returns KMC_ERR_CAPACITY if any call on the device raised it
+ * since the last query, KMC_OK otherwise, and clears it; a dense call that finds
+ * the flag raised at entry also returns KMC_ERR_CAPACITY (and clears it), as does
+ * kmc_count_multi after its synchronisation. */
+KMC_API int kmc_dense_status(int device);
 
 /* ------------------------------------------------------------------------ */
 /* Sharding.  A shard counts the windows starting in
@@ -137,7 +156,7 @@ typedef struct kmc_shard {
     uint64_t read_lo, read_hi;
 } kmc_shard;
 
-int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, int nshards, uint64_t align,
+KMC_API int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, int nshards, uint64_t align,
                     kmc_shard *out);
 
 /* Single-process multi-GPU count of a host buffer (the C++ host driver's path):
@@ -147,15 +166,18 @@ int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, int nshard
  * sum[s + num_seqs*code] (and optional invalid[s]) is copied back to host
  * memory.  devices == NULL -> 0 .. ndev-1 (distinct devices).  Synchronous.
  * One host thread per device streams its shard through pinned staging buffers,
- * so all devices load concurrently.  The RCCL communicators of a device set are
- * created on its first call and reused until kmc_multi_release().  Thread-safe:
- * concurrent calls on the same device set take turns for the collective (RCCL
- * communicators are not reentrant), calls on disjoint sets run concurrently, and
- * a set whose collective failed is rebuilt by the next call. */
-int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes, int k,
+ * so all devices load concurrently.  The RCCL communicators of a device set (keyed
+ * by the sorted device list) are created on its first call, and each device's
+ * stream, pinned staging and device buffers (grow-only) on its first use; all are
+ * reused until kmc_multi_release().  Thread-safe: a call holds its devices (locked
+ * in ascending order) from load to copy-back, so calls whose sets share a device
+ * take turns (RCCL communicators are not reentrant), calls on disjoint sets run
+ * concurrently, and a set whose collective failed is rebuilt by the next call. */
+KMC_API int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes, int k,
                     int ndev, const int *devices, int32_t *sum, int32_t *invalid);
-/* Destroys the communicators cached by kmc_count_multi. */
-int kmc_multi_release(void);
+/* Destroys the communicators and frees the per-device state cached by
+ * kmc_count_multi (waits for calls in flight). */
+KMC_API int kmc_multi_release(void);
 
 /* ------------------------------------------------------------------------ */
 /* Pairwise k-mer distance (the reference's step 2).
@@ -175,8 +197,8 @@ int kmc_multi_release(void);
  *   workspace device scratch of kmc_pair_distances_workspace_size() bytes (0 when
  *             the pair matrix alone fills the GPU), or NULL for a library buffer
  * Exact while every record has fewer than 2^32 windows. */
-size_t kmc_pair_distances_workspace_size(uint64_t num_seqs, int k, int device);
-int kmc_pair_distances(const int32_t *sum, uint64_t sum_ld, const int64_t *indices, uint64_t num_seqs, int k,
+KMC_API size_t kmc_pair_distances_workspace_size(uint64_t num_seqs, int k, int device);
+KMC_API int kmc_pair_distances(const int32_t *sum, uint64_t sum_ld, const int64_t *indices, uint64_t num_seqs, int k,
                        float *out, void *workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Exact drop-in for one reference launch
@@ -185,7 +207,7 @@ int kmc_pair_distances(const int32_t *sum, uint64_t sum_ld, const int64_t *indic
  * current_seq to every later record, 4^KMC_DROPIN_K codes, summed in float in
  * code order as kernels.h:103 does (so bit-identical to the reference kernel
  * also when that float sum rounds).  Device int sums/indexes, float mins. */
-int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq, int *indexes, hipStream_t stream);
+KMC_API int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq, int *indexes, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Canonical k-mer counting, k <= 31 (BASELINE config C4).  No
@@ -203,16 +225,30 @@ int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq, int *i
  * unspecified), rec_offsets device uint64[num_seqs + 1]; *num_distinct (host) =
  * rec_offsets[num_seqs].  If capacity < *num_distinct nothing is written except
  * rec_offsets and KMC_ERR_CAPACITY is returned (valid windows, <= data bytes,
- * always suffice).  data 16-byte aligned with data[p] = byte p of the global
- * offsets in `indices` (device int64[num_seqs + 1]).  Synchronous on `stream`
- * (the distinct total is returned to the host); workspace memory is
- * library-owned, about 20 bytes per window (no hash table lives in HBM). */
+ * always suffice).  data (any alignment, like the dense entry points) with
+ * data[p] = byte p of the global offsets in `indices` (device int64[num_seqs + 1]).
+ * Synchronous on `stream` (the distinct total is returned to the host).  The
+ * workspace, about 20 bytes per window (no hash table lives in HBM), is
+ * library-owned here (one per device, grown on demand, shared by the calls on that
+ * device, which must not overlap); kmc_count_canonical_hash_ex takes the caller's
+ * instead, of kmc_count_canonical_workspace_size() bytes (NULL: library-owned). */
 #define KMC_CANON_MAX_K 31
 #define KMC_CANON_SOFTMASK 1u
 #define KMC_CANON_FORWARD 2u
-int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k, unsigned flags,
+KMC_API int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t num_seqs, int k, unsigned flags,
                              uint64_t *keys, uint32_t *counts, uint64_t capacity, uint64_t *rec_offsets,
                              uint64_t *num_distinct, hipStream_t stream);
+/* Workspace bytes of a canonical call over records with these offsets (HOST
+ * int64[num_seqs + 1], the same values as the call's device `indices`), on
+ * `device`, valid for any alignment of `data`; 0 on bad arguments. */
+KMC_API size_t kmc_count_canonical_workspace_size(const int64_t *host_indices, uint64_t num_seqs, int k, int device);
+/* kmc_count_canonical_hash with a caller workspace (KMC_ERR_WORKSPACE when smaller
+ * than the size above; NULL = the library-owned one).  Calls with their own
+ * workspaces may run concurrently on different streams. */
+KMC_API int kmc_count_canonical_hash_ex(const char *data, const int64_t *indices, uint64_t num_seqs, int k,
+                                        unsigned flags, uint64_t *keys, uint32_t *counts, uint64_t capacity,
+                                        uint64_t *rec_offsets, uint64_t *num_distinct, void *workspace,
+                                        size_t workspace_bytes, hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Tracing (the reference times step 1 with cudaEvents, main.cu:262-300): when set,
@@ -223,17 +259,19 @@ int kmc_count_canonical_hash(const char *data, const int64_t *indices, uint64_t 
 #define KMC_HIP_EVENT_T_DEFINED
 typedef struct ihipEvent_t *hipEvent_t; /* identical to HIP's own typedef */
 #endif
-int kmc_trace_set_events(hipEvent_t before, hipEvent_t after);
+KMC_API int kmc_trace_set_events(hipEvent_t before, hipEvent_t after);
 
 /* ------------------------------------------------------------------------ */
 /* Launch shaping for overlapped collectives (no reference counterpart): the k <= 8
  * dense kernel runs one 1024-thread workgroup per CU over static byte ranges, so a
  * CU that another kernel holds when a count starts (an RCCL all-reduce overlapping
  * the next step, bench.py at N > 1) delays the whole launch.  With n > 0 the
- * following dense calls of the process launch n workgroups fewer, leaving n CUs to
- * the concurrent kernel (0 <= n <= 64; 0 = every CU, the default).  The workspace
- * size depends on it: query kmc_count_dense_ex_workspace_size after setting it. */
-int kmc_set_reserved_cus(int n);
+ * following dense calls issued from this host thread (like kmc_trace_set_events,
+ * the setting is per thread: other threads' calls are unaffected) launch n
+ * workgroups fewer, leaving n CUs to the concurrent kernel (0 <= n <= 64; 0 =
+ * every CU, the default).  The workspace size depends on it: query
+ * kmc_count_dense_ex_workspace_size after setting it, on the same thread. */
+KMC_API int kmc_set_reserved_cus(int n);
 
 /* ------------------------------------------------------------------------ */
 /* Synthetic input generator (benchmark layout): num_records
@@ -241,15 +279,15 @@ int kmc_set_reserved_cus(int n);
  * first_base + r*record_len + i) is "ACGT"[(x_{g/32} >> 2*(g%32)) & 3] where x_n
  * is output n of splitmix64 seeded with `seed`.  Writes num_records*(record_len+1)
  * bytes.  kmc_synth_indices fills the matching int64 offsets on the host. */
-int kmc_synth_fill(char *data, uint64_t num_records, uint64_t record_len, uint64_t seed,
+KMC_API int kmc_synth_fill(char *data, uint64_t num_records, uint64_t record_len, uint64_t seed,
                    uint64_t first_base, hipStream_t stream);
-void kmc_synth_indices(int64_t *indices, uint64_t num_records, uint64_t record_len);
+KMC_API void kmc_synth_indices(int64_t *indices, uint64_t num_records, uint64_t record_len);
 /* Bytes [lo, hi) of the same record stream with first_base = 0 (record r occupies
  * global bytes [r*(record_len+1), (r+1)*(record_len+1)), its last one '\0'),
  * written to data[0 .. hi-lo): what a rank of a strong-scaled job holds of the
  * one global buffer (its shard and halo) without generating whole records.
  * data 16-byte aligned; lo need not be. */
-int kmc_synth_fill_range(char *data, uint64_t lo, uint64_t hi, uint64_t record_len, uint64_t seed,
+KMC_API int kmc_synth_fill_range(char *data, uint64_t lo, uint64_t hi, uint64_t record_len, uint64_t seed,
                          hipStream_t stream);
 
 /* ------------------------------------------------------------------------ */
@@ -265,16 +303,16 @@ int kmc_synth_fill_range(char *data, uint64_t lo, uint64_t hi, uint64_t record_l
  * each record ends with '\0') and always carries num_seqs + 1 offsets. */
 typedef struct kmc_fasta kmc_fasta;
 
-int kmc_fasta_load(const char *path, int dialect, int64_t max_seqs, kmc_fasta **out);
-uint64_t kmc_fasta_num_seqs(const kmc_fasta *f);
-const int64_t *kmc_fasta_indices(const kmc_fasta *f); /* num_seqs + 1 entries */
-const char *kmc_fasta_data(const kmc_fasta *f);
-uint64_t kmc_fasta_data_bytes(const kmc_fasta *f);
+KMC_API int kmc_fasta_load(const char *path, int dialect, int64_t max_seqs, kmc_fasta **out);
+KMC_API uint64_t kmc_fasta_num_seqs(const kmc_fasta *f);
+KMC_API const int64_t *kmc_fasta_indices(const kmc_fasta *f); /* num_seqs + 1 entries */
+KMC_API const char *kmc_fasta_data(const kmc_fasta *f);
+KMC_API uint64_t kmc_fasta_data_bytes(const kmc_fasta *f);
 /* Number of entries the reference's indexes_aux would hold: num_seqs + 1, or
  * num_seqs when the input ends in a blank line (the reference then drops the end
  * sentinel and its kernel reads out of bounds). */
-uint64_t kmc_fasta_reference_num_indexes(const kmc_fasta *f);
-void kmc_fasta_free(kmc_fasta *f);
+KMC_API uint64_t kmc_fasta_reference_num_indexes(const kmc_fasta *f);
+KMC_API void kmc_fasta_free(kmc_fasta *f);
 
 /* FASTA parsing on the GPU: the record rules of
  * kmc_fasta_load (importSeqs / importSeqsNoNL, main.cu:474-545 / 401-473) without
@@ -286,7 +324,7 @@ void kmc_fasta_free(kmc_fasta *f);
  * On return *num_seqs and *data_bytes describe the buffer exactly as
  * kmc_fasta_load would; KMC_ERR_CAPACITY (with *num_seqs set) when indices_cap <
  * *num_seqs + 1.  Synchronous on `stream`; library-owned scratch (~2 B per line). */
-int kmc_fasta_parse_device(const char *raw, uint64_t raw_bytes, int dialect, char *data, uint64_t data_cap,
+KMC_API int kmc_fasta_parse_device(const char *raw, uint64_t raw_bytes, int dialect, char *data, uint64_t data_cap,
                            int64_t *indices, uint64_t indices_cap, uint64_t *num_seqs, uint64_t *data_bytes,
                            hipStream_t stream);
 
@@ -297,7 +335,7 @@ int kmc_fasta_parse_device(const char *raw, uint64_t raw_bytes, int dialect, cha
  * loaded by kmc_fasta_load and copied instead.  *data (*data_bytes + 16 bytes) and
  * *indices (*num_seqs + 1 entries) are hipMalloc'ed; the caller hipFree's them.
  * Synchronous on `stream`. */
-int kmc_fasta_load_device(const char *path, int dialect, int64_t max_seqs, char **data, uint64_t *data_bytes,
+KMC_API int kmc_fasta_load_device(const char *path, int dialect, int64_t max_seqs, char **data, uint64_t *data_bytes,
                           int64_t **indices, uint64_t *num_seqs, hipStream_t stream);
 
 #ifdef __cplusplus

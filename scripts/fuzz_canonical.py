@@ -4,7 +4,6 @@
 flags and K4 claim capacities (the test hook), bit-exact per record.
 Usage: python scripts/fuzz_canonical.py [--cases 40] [--seed 1]"""
 import argparse
-import ctypes
 import os
 import sys
 
@@ -43,8 +42,7 @@ def main():
     import kmc
     import oracle
     dev = torch.device("cuda:0")
-    hook = kmc.lib().kmc_diag_canon_claim_cap
-    hook.argtypes = [ctypes.c_uint]
+    hook = kmc.diag().__enter__().kmc_diag_canon_claim_cap  # diagnostic library (test hooks)
     rng = np.random.default_rng(a.seed)
     bad = 0
     for c in range(a.cases):

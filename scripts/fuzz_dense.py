@@ -47,6 +47,8 @@ def main():
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(a.seed)
     bad = 0
+    if a.sampled:  # the mode hook lives in the diagnostic library (lib/libkmc_diag.so)
+        kmc.diag().__enter__()
     for c in range(a.cases):
         k = int(rng.integers(1, 14))
         data, idx = make_case(rng, k)

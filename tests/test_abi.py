@@ -1,5 +1,6 @@
 """The C-ABI library loads on a CPU-only host and exports what include/kmc.h declares."""
 import ctypes
+import subprocess
 
 import numpy as np
 
@@ -11,6 +12,31 @@ def test_library_exports_every_header_symbol(kmc):
     L = kmc.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
+
+
+def _dynamic_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return sorted(l.split()[-1] for l in out.splitlines() if l.strip())
+
+
+def test_library_exports_exactly_the_header(kmc):
+    """libkmc.so (hidden visibility + libkmc.map) exports exactly kmc.h's entry points:
+    no test hook, no internal or C++ symbol that another caller could bind to."""
+    assert _dynamic_symbols(kmc.LIB_PATH) == kmc.header_symbols()
+
+
+def test_diag_library_adds_only_the_test_hooks(kmc):
+    """lib/libkmc_diag.so: the same entry points plus the kmc_diag_* hooks."""
+    got = _dynamic_symbols(kmc.DIAG_LIB_PATH)
+    hooks = [n for n in got if n.startswith("kmc_diag_")]
+    assert hooks == ["kmc_diag_canon_claim_cap", "kmc_diag_canon_sort_cap", "kmc_diag_dense_spill_cap",
+                     "kmc_diag_radix_mode"]
+    assert sorted(set(got) - set(hooks)) == kmc.header_symbols()
+    assert kmc.lib() is not None
+    with kmc.diag() as D:  # inside diag() every binding uses the diagnostic library
+        assert kmc.lib() is D and D.kmc_diag_radix_mode(1, 1.0) == 0
+    assert not hasattr(kmc.lib(), "kmc_diag_radix_mode")
+    assert kmc.lib().kmc_dense_status(0) == 0  # no device touched: nothing raised
 
 
 def test_error_strings_and_version(kmc):
@@ -28,15 +54,22 @@ def test_argument_errors_need_no_device(kmc):
     assert L.kmc_count_dense(None, None, 0, 0, 3, None, None, None, 0, None) == 0
     assert L.sumKmereCoincidencesGlobalMemory_hip(None, None, 0, None, None) == 0
     assert L.sumKmereCoincidencesGlobalMemory_hip(None, None, 3, None, None) == 1001
-    # the canonical counter still needs a 16-byte aligned data pointer: refused
-    # before any device call (the dense entry points take any pointer, like
-    # kernels.h:113: tests/test_dense_gpu.py runs them on data + 1 .. 15)
+    # the canonical counter takes any data pointer (since round 4, like the dense
+    # entry points): a misaligned one is not refused, null offsets are
     buf = (ctypes.c_char * 64)()
     base = ctypes.addressof(buf)
     mis = ctypes.c_void_p(base + (1 if base % 16 == 0 else 0) + (16 - base % 16) % 16)
     nd = ctypes.c_uint64(0)
-    assert L.kmc_count_canonical_hash(mis, ctypes.c_void_p(base), 1, 21, 0, None, None, 0, ctypes.c_void_p(base),
-                                      ctypes.byref(nd), None) == 1003
+    assert L.kmc_count_canonical_hash(mis, None, 1, 21, 0, None, None, 0, ctypes.c_void_p(base),
+                                      ctypes.byref(nd), None) == 1001
+    assert L.kmc_count_canonical_hash_ex(mis, None, 1, 21, 0, None, None, 0, ctypes.c_void_p(base),
+                                         ctypes.byref(nd), None, 0, None) == 1001
+    assert L.kmc_count_canonical_hash(mis, None, 1, 32, 0, None, None, 0, None, ctypes.byref(nd), None) == 1002
+    # size query: host offsets, bad arguments give 0 (no device needed for those)
+    idx = np.array([0, 100, 50], dtype=np.int64)  # decreasing: refused
+    assert L.kmc_count_canonical_workspace_size(idx.ctypes.data_as(ctypes.c_void_p), 2, 21, 0) == 0
+    assert L.kmc_count_canonical_workspace_size(None, 2, 21, 0) == 0
+    assert L.kmc_count_canonical_workspace_size(idx.ctypes.data_as(ctypes.c_void_p), 1, 40, 0) == 0
 
 
 def test_synth_indices_and_host_generator(kmc):

@@ -207,10 +207,12 @@ def test_radix_wrapping_bins_recounted(kmc, oracle, cuda, k):
 def radix_mode(kmc):
     """kmc_diag_radix_mode(mode, cap_scale): 0 auto, 1 exact offsets, 2 sampled
     regions; cap_scale < 1 shrinks the sampled capacities so regions overflow and
-    the gated exact rerun takes over.  Restored to auto afterwards."""
-    hook = kmc.lib().kmc_diag_radix_mode
-    yield hook
-    assert hook(0, 1.0) == 0
+    the gated exact rerun takes over.  The hook exists only in the diagnostic
+    library (lib/libkmc_diag.so), which every binding uses inside kmc.diag();
+    restored to auto afterwards."""
+    with kmc.diag() as D:
+        yield D.kmc_diag_radix_mode
+        assert D.kmc_diag_radix_mode(0, 1.0) == 0
 
 
 @pytest.mark.parametrize("k", [9, 10, 11, 12, 13])
@@ -533,12 +535,61 @@ def test_count_multi_single_device(kmc, oracle, cuda):
     got, _ = kmc.count_multi(big, bidx, 4, ndev=1, devices=[0])
     exp, _ = oracle.count_dense(big, bidx, 4)
     np.testing.assert_array_equal(got, exp)
+    # the cached buffers are grow-only: a smaller shard with a larger count matrix
+    # (data buffer reused, sum buffer grown) and the invalid vector after a call without it
+    many, midx = random_records(rng, [3_000] * 40, 0.01, 0.01)
+    got, inv = kmc.count_multi(many, midx, 8, ndev=1, invalid=True)
+    exp, exp_inv = oracle.count_dense(many, midx, 8)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+    got, _ = kmc.count_multi(big, bidx, 4, ndev=1)
+    exp, _ = oracle.count_dense(big, bidx, 4)
+    np.testing.assert_array_equal(got, exp)
     assert kmc.lib().kmc_multi_release() == 0
+    assert kmc.lib().kmc_multi_release() == 0  # idempotent
     got, _ = kmc.count_multi(data, idx, 3, ndev=1)
     exp, _ = oracle.count_dense(data, idx, 3)
     np.testing.assert_array_equal(got, exp)
     with pytest.raises(kmc.KmcError):  # one communicator rank per device
         kmc.count_multi(data, idx, 3, ndev=2, devices=[0, 0])
+
+
+def test_dense_spill_overflow_raises_status(kmc, oracle, cuda):
+    """k = 8 spill lists past their capacity are never silent: with the capacity
+    lowered to 1 entry (diagnostic library) a 64 MB poly-A record (every workgroup's
+    piece wraps its AAAAAAAA counter ~4 times: several wrap entries each) raises the
+    host-mapped flag, which kmc_dense_status reports once and clears, and which the
+    next dense call reports at entry; with the capacity restored the counts are the
+    oracle's and nothing is raised."""
+    import torch
+    rng = np.random.default_rng(404)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    recs = [np.append(np.full(64 << 20, ord("A"), np.uint8), np.uint8(0)),
+            np.append(acgt[rng.integers(0, 4, 1_000_000)], np.uint8(0))]
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    exp, exp_inv = oracle.count_dense(data, idx, 8)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    dv = torch.cuda.current_device()
+    with kmc.diag() as D:
+        assert D.kmc_dense_status(dv) == 0
+        assert D.kmc_diag_dense_spill_cap(1) == 0
+        kmc.count_dense(d, di, 8, data_bytes=data.size)
+        torch.cuda.synchronize()
+        assert D.kmc_dense_status(dv) == 1009
+        assert D.kmc_dense_status(dv) == 0  # reported once
+        kmc.count_dense(d, di, 8, data_bytes=data.size)
+        torch.cuda.synchronize()
+        with pytest.raises(kmc.KmcError) as e:  # the next call reports it at entry
+            kmc.count_dense(d, di, 8, data_bytes=data.size)
+        assert e.value.code == 1009
+        assert D.kmc_diag_dense_spill_cap(0) == 0
+        out, inv = kmc.count_dense(d, di, 8, data_bytes=data.size, invalid=True)
+        torch.cuda.synchronize()
+        assert D.kmc_dense_status(dv) == 0
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv)
+    assert kmc.lib().kmc_dense_status(dv) == 0
 
 
 def test_synth_fill_range_matches_host(kmc, cuda):

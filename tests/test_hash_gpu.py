@@ -123,16 +123,12 @@ def test_canonical_pass_overflow_split(kmc, oracle, cuda, cap):
     rep = np.frombuffer(b"ACGTTGCA" * 100_000 + b"A" * 200_000, dtype=np.uint8)
     data = np.concatenate([data, rep, np.zeros(1, np.uint8)])
     idx = np.append(idx, data.size)
-    hook = kmc.lib().kmc_diag_canon_claim_cap
-    hook.argtypes = [ctypes.c_uint]
-    sort_cap = kmc.lib().kmc_diag_canon_sort_cap  # 0: every list to the table kernel
-    sort_cap.argtypes = [ctypes.c_uint]
-    assert hook(cap) == 0 and sort_cap(0) == 0
-    try:
+    with kmc.diag() as D:  # the hooks live in the diagnostic library only
+        hook = D.kmc_diag_canon_claim_cap
+        sort_cap = D.kmc_diag_canon_sort_cap  # 0: every list to the table kernel
+        assert hook(cap) == 0 and sort_cap(0) == 0
         for k in (21, 31):
             assert_same(gpu_canon(kmc, cuda, data, idx, k), oracle.count_canonical(data, idx, k), "cap=%d k=%d" % (cap, k))
-    finally:
-        assert hook(0) == 0 and sort_cap(1 << 30) == 0
 
 
 @pytest.mark.parametrize("scap", [0, 1, 2500, 1 << 30])
@@ -149,17 +145,13 @@ def test_canonical_sort_and_table_paths(kmc, oracle, cuda, scap):
     rep = np.frombuffer(b"ACGTTGCAAT" * 3000 + b"G" * 900 + b"ACGATCGATCGGA" * 400, dtype=np.uint8)
     data = np.concatenate([data, rep, np.zeros(1, np.uint8)])
     idx = np.append(idx, data.size)
-    sort_cap = kmc.lib().kmc_diag_canon_sort_cap
-    sort_cap.argtypes = [ctypes.c_uint]
-    assert sort_cap(scap) == 0
-    try:
+    with kmc.diag() as D:  # the hook lives in the diagnostic library only
+        assert D.kmc_diag_canon_sort_cap(scap) == 0
         for k in (17, 31):
             for flags in (0, kmc.CANON_SOFTMASK):
                 got = gpu_canon(kmc, cuda, data, idx, k, flags)
                 exp = oracle.count_canonical(data, idx, k, soft=bool(flags & 1))
                 assert_same(got, exp, "scap=%d k=%d flags=%d" % (scap, k, flags))
-    finally:
-        assert sort_cap(1 << 30) == 0
 
 
 def test_canonical_crowded_list_deferred(kmc, oracle, cuda):
@@ -235,3 +227,36 @@ def test_canonical_repeat_rich_genome(kmc, oracle, cuda, k, soft):
     if soft:  # the repeat path is exercised (unmasked: the lowercase repeats are not bases)
         assert exp[1].max() > 1000 and (exp[1] > 1).sum() > 100_000
     assert_same(got, exp, "repeat-rich k=%d soft=%s" % (k, soft))
+
+
+@pytest.mark.parametrize("k", [11, 31])
+def test_canonical_unaligned_data_and_caller_workspace(kmc, oracle, cuda, k):
+    """The canonical entry point takes any data pointer (rounded down to 16 bytes,
+    offsets biased, as the dense path does): data + 1, 7, 8, 15 of a buffer give the
+    self-oracle's counts; kmc_count_canonical_hash_ex with a caller workspace of the
+    queried size gives the same, and a workspace one byte short is refused."""
+    import torch
+    rng = np.random.default_rng(900 + k)
+    data, idx = random_records(rng, [0, 5, 40_000, 1, 333_333, 64], b"ACGTNacgt",
+                               (.2, .2, .2, .2, .04, .04, .04, .04, .04))
+    exp = oracle.count_canonical(data, idx, k, soft=True)
+    di = dev(idx, cuda)
+    for off in (1, 7, 8, 15):
+        big = torch.zeros(data.size + 48, dtype=torch.uint8, device=cuda)
+        big[off:off + data.size] = dev(data, cuda)
+        d = big[off:off + data.size]
+        keys, counts, ro = kmc.count_canonical(d, di, k, flags=kmc.CANON_SOFTMASK, capacity=data.size)
+        torch.cuda.synchronize()
+        got = (keys.cpu().numpy().view(np.uint64), counts.cpu().numpy().view(np.uint32), ro.cpu().numpy())
+        assert_same(got, exp, "offset %d" % off)
+        wsb = kmc.canonical_workspace_size(idx, k, torch.cuda.current_device())
+        assert wsb > 0
+        ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+        keys, counts, ro = kmc.count_canonical(d, di, k, flags=kmc.CANON_SOFTMASK, capacity=data.size,
+                                               workspace=ws)
+        torch.cuda.synchronize()
+        got = (keys.cpu().numpy().view(np.uint64), counts.cpu().numpy().view(np.uint32), ro.cpu().numpy())
+        assert_same(got, exp, "caller workspace, offset %d" % off)
+    with pytest.raises(kmc.KmcError) as e:
+        kmc.count_canonical(d, di, k, flags=kmc.CANON_SOFTMASK, capacity=data.size, workspace=ws[:wsb - 1])
+    assert e.value.code == 1004

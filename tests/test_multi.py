@@ -212,6 +212,8 @@ def _bench_step_worker(rank, world, port, scaling, records, L, k, steps, q):
     (4, "strong", 3, 1_000, 3),   # 3003 bytes < one 4 KiB cut: three empty shards
     (2, "weak", 3, 5_000, 8),
     (4, "weak", 2, 3_000, 5),
+    (8, "weak", 10, 2_000, 8),    # C5's plan: 10 records per rank, 8 ranks
+    (8, "strong", 10, 20_000, 8),  # the headline's plan at 8 ranks (cuts inside records)
 ])
 def test_gloo_bench_step_driver(world, scaling, records, L, k):
     res = _spawn(_bench_step_worker, world, scaling, records, L, k, 3)
