@@ -132,6 +132,9 @@ struct HParams {
     uint32_t *err;           // set when a list exceeds what K4 can split
     uint32_t claim_cap;      // K4 claims per wave and pass (kClaimW; smaller only in tests)
     uint32_t sort_cap;       // K4s takes lists of at most this many keys (kSortCap; 0 in tests: none)
+    uint32_t sort_cap_big;   // the big K4s instance takes the longer ones up to this (kSortCapBig; 0: none)
+    uint64_t *big;           // [lists][3] (list, begin, end) handed by K4s to its big instance
+    unsigned long long *nbig;  // their number
     uint64_t *defer;         // [lists][3] (list, begin, end) left to the table kernel by K4s
     unsigned long long *ndefer;  // their number
     uint64_t *rec_off;       // [n + 1] output offsets
@@ -891,35 +894,53 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
 // A list that does not fit (longer than sort_cap, or a slot holding more than
 // kSortMaxM keys: a key repeated that often) is appended to p.defer and counted by
 // canon_table_kernel, which handles any length and any repeat count.
-constexpr int kSortBlock = 512;
-constexpr int kSortRes = 12;                          // keys per thread
-constexpr uint32_t kSortCap = 6080;                   // <= kSortBlock * kSortRes; LDS: 2 workgroups per CU
-constexpr int kSortSlotsLg = 13;
-constexpr int kSortSlots = 1 << kSortSlotsLg;         // 16-bit counters, two per word
+// Two instances (round 4): the common one, two 512-thread workgroups per CU, takes
+// lists of up to 6 080 keys; a big one, one 1 024-thread workgroup per CU with a
+// 16 384-slot counter table, takes the lists of 6 081 .. 12 288 keys that the
+// first hands it (chromosome-sized records: 2^15 lists of ~7.6 K keys), which
+// until round 3 went to the probed table kernel.
+template <int BLOCK, int RES, uint32_t CAP, int SLOTS_LG>
+struct SortCfg {
+    static constexpr int kBlock = BLOCK;
+    static constexpr int kRes = RES;                    // keys per thread
+    static constexpr uint32_t kCap = CAP;               // <= kBlock * kRes
+    static constexpr int kSlotsLg = SLOTS_LG;
+    static constexpr int kSlots = 1 << SLOTS_LG;        // 16-bit counters, two per word
+    static_assert(CAP <= (uint32_t)(BLOCK * RES) && CAP < 65536u, "K4s sizes");
+    static_assert(kSlots / 2 == BLOCK * 8, "K4s scan: 8 counter words per thread");
+};
+using SortSmall = SortCfg<512, 12, 6080, 13>;   // LDS: 2 workgroups per CU
+using SortBig = SortCfg<1024, 12, 12288, 14>;   // LDS: 1 workgroup per CU
+constexpr int kSortBlock = SortSmall::kBlock;
+constexpr uint32_t kSortCap = SortSmall::kCap;
+constexpr uint32_t kSortCapBig = SortBig::kCap;
 #ifndef KMC_SORT_MAXM
 #define KMC_SORT_MAXM 8
 #endif
 constexpr uint32_t kSortMaxM = KMC_SORT_MAXM;         // keys per slot handled by the pairwise dedup
 constexpr uint32_t kHotMax = 128;                     // crowded slots per list handled by wave rounds
-static_assert(kSortCap <= (uint32_t)(kSortBlock * kSortRes) && kSortCap < 65536u, "K4s sizes");
-static_assert(kSortSlots / 2 == kSortBlock * 8, "K4s scan: 8 counter words per thread");
 
+template <class C>
 struct K4sLds {
-    unsigned long long sk[kSortCap];  // the list, sorted by slot
-    uint32_t sc[kSortSlots / 2];      // slot counters, then slot starts (16-bit, packed)
+    unsigned long long sk[C::kCap];   // the list, sorted by slot
+    uint32_t sc[C::kSlots / 2];       // slot counters, then slot starts (16-bit, packed)
     uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
-    uint16_t q[kSortBlock / 64][kSortRes * 64];  // per wave: positions of keys that share a slot
-    uint32_t wsum[kSortBlock / 64];
+    uint16_t q[C::kBlock / 64][C::kRes * 64];  // per wave: positions of keys that share a slot
+    uint32_t wsum[C::kBlock / 64];
     uint32_t out;                     // distinct keys emitted
     uint32_t nhot;
 };
+static_assert(sizeof(K4sLds<SortBig>) <= 160 * 1024, "big K4s instance: one workgroup per CU");
 
-// a list left to the table kernel: its id and key range
+// a list left to another kernel: its id and key range, appended to (q, nq)
+__device__ __forceinline__ void queue_list(uint64_t *q, unsigned long long *nq, int64_t l, uint64_t b, uint64_t e) {
+    const unsigned long long i = atomicAdd(nq, 1ull);
+    q[3 * i] = (uint64_t)l;
+    q[3 * i + 1] = b;
+    q[3 * i + 2] = e;
+}
 __device__ __forceinline__ void defer_list(const HParams &p, int64_t l, uint64_t b, uint64_t e) {
-    const unsigned long long i = atomicAdd(p.ndefer, 1ull);
-    p.defer[3 * i] = (uint64_t)l;
-    p.defer[3 * i + 1] = b;
-    p.defer[3 * i + 2] = e;
+    queue_list(p.defer, p.ndefer, l, b, e);
 }
 
 // The pair format (K4s, K4 -> K5): a canonical key of k <= 31 bases uses at most
@@ -938,183 +959,211 @@ __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned
 __device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t hi) { return hi ? (w >> 16) : (w & 0xFFFFu); }
 
 
-// start of slot sl's keys in sk (after the scan); slot kSortSlots ends at n
-__device__ __forceinline__ uint32_t slot_start(const K4sLds &S, uint32_t sl, uint32_t n) {
-    return sl < (uint32_t)kSortSlots ? half16(S.sc[sl >> 1], sl & 1u) : n;
+// start of slot sl's keys in sk (after the scan); slot kSlots ends at n
+template <class C>
+__device__ __forceinline__ uint32_t slot_start(const K4sLds<C> &S, uint32_t sl, uint32_t n) {
+    return sl < (uint32_t)C::kSlots ? half16(S.sc[sl >> 1], sl & 1u) : n;
 }
 
-__global__ __launch_bounds__(kSortBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_sort_kernel(HParams p) {
-    __shared__ __attribute__((aligned(16))) K4sLds S;
+// One list of n <= C::kCap keys [b0, e0) counted by the counting sort (the
+// workgroup calls it uniformly).  A list with too many crowded slots is deferred
+// to the table kernel.
+template <class C>
+__device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_t l, uint64_t b0, uint64_t e0,
+                                          uint32_t n) {
+    constexpr int kRes = C::kRes, kBlk = C::kBlock, kSlots = C::kSlots;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint64_t lt = (1ull << lane) - 1ull;
     uint16_t *wq = S.q[wv];
+    unsigned long long kh[kRes];
+#pragma unroll
+    for (int j = 0; j < kRes; ++j) {
+        const uint32_t i = (uint32_t)(j * kBlk + tid);
+        kh[j] = i < n ? p.ent[b0 + i] : kEmptyH;
+    }
+    reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
+    lds_barrier();  // A: counters zero; the previous list is done
+    if (tid == 0) {
+        S.out = 0u;
+        S.nhot = 0u;
+    }
+    // rank: one returning add per key on its slot's 16-bit counter
+    uint32_t rk[kRes / 2];  // ranks (< 2^16), two per register
+#pragma unroll
+    for (int j = 0; j < kRes; ++j) {
+        if ((j & 1) == 0) rk[j >> 1] = 0u;
+        if ((uint32_t)(j * kBlk + tid) < n) {
+            const uint32_t sl = (uint32_t)kh[j] & (kSlots - 1);
+            const uint32_t o = __hip_atomic_fetch_add(&S.sc[sl >> 1], (sl & 1u) ? 0x10000u : 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            rk[j >> 1] |= half16(o, sl & 1u) << (16 * (j & 1));
+        }
+    }
+    lds_barrier();  // B: every key ranked
+    // scan: thread t owns counter words 8t .. 8t+7 (slots 16t .. 16t+15)
+    const uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
+    const uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
+    uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    uint32_t run = 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t c0 = w[i] & 0xFFFFu, c1 = w[i] >> 16;
+        if (__builtin_expect(c0 > kSortMaxM, 0)) {
+            const uint32_t x = atomicAdd(&S.nhot, 1u);
+            if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i;
+        }
+        if (__builtin_expect(c1 > kSortMaxM, 0)) {
+            const uint32_t x = atomicAdd(&S.nhot, 1u);
+            if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i + 1u;
+        }
+        w[i] = run | ((run + c0) << 16);  // exclusive starts, relative to the thread
+        run += c0 + c1;
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) S.wsum[wv] = incl;
+    lds_barrier();  // C1: wave totals
+    uint32_t base = incl - run;
+#pragma unroll
+    for (int v = 0; v < kBlk / 64; ++v) base += v < wv ? S.wsum[v] : 0u;
+    const uint32_t bb = base | (base << 16);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] += bb;  // starts < 2^16: no carry between the halves
+    reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
+    reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+    lds_barrier();  // C2: slot starts
+    const uint32_t nhot = S.nhot;
+    if (nhot > kHotMax) {  // too many crowded slots: the probed table counts this list (uniform)
+        if (tid == 0) defer_list(p, l, b0, e0);
+        return;  // (the next list's barrier A orders the LDS reuse)
+    }
+    // scatter: a key alone in its slot (the common case: ~4 K keys over 8 192
+    // slots) is a distinct key of count 1 and leaves at once; the others go to
+    // sk, and those of slots with at most kSortMaxM keys to this wave's queue
+    // of keys to check against their slot
+    uint32_t qn = 0u;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < kRes; ++j) {
+        bool alone = false, shared = false;
+        uint32_t pos = 0u;
+        if ((uint32_t)(j * kBlk + tid) < n) {
+            const uint32_t sl = (uint32_t)kh[j] & (kSlots - 1);
+            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
+            const uint32_t m = slot_start(S, sl + 1u, n) - a;
+            pos = a + half16(rk[j >> 1], j & 1);
+            alone = m == 1u;
+            if (!alone) {
+                S.sk[pos] = kh[j];
+                shared = m <= kSortMaxM;
+            }
+        }
+        const uint64_t am = __ballot(alone);
+        if (am) {
+            uint32_t wb = 0u;
+            if (lane == 0) wb = atomicAdd(&S.out, (uint32_t)__popcll(am));
+            wb = (uint32_t)__shfl((int)wb, 0);
+            if (alone) emit_pair(p, b0 + wb + (uint32_t)__popcll(am & lt), kh[j], 1u);
+        }
+        const uint64_t sm = __ballot(shared);
+        if (shared) wq[qn + (uint32_t)__popcll(sm & lt)] = (uint16_t)pos;
+        qn += (uint32_t)__popcll(sm);
+    }
+    lds_barrier();  // D: the shared keys sorted by slot
+    // the wave's queued keys, 64 at a time: the first occurrence in its slot is
+    // emitted with the slot's count of its key
+    for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
+        const bool act = q0 + (uint32_t)lane < qn;
+        bool first = false;
+        uint32_t cnt = 1u;
+        unsigned long long h = 0;
+        if (act) {
+            const uint32_t pos = wq[q0 + lane];
+            h = S.sk[pos];
+            const uint32_t sl = (uint32_t)h & (kSlots - 1);
+            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
+            first = true;
+            for (uint32_t q = a; q < e; ++q) {  // 2 <= m <= kSortMaxM
+                if (q != pos && S.sk[q] == h) {
+                    ++cnt;
+                    first = first && q > pos;
+                }
+            }
+        }
+        const uint64_t m = __ballot(first);
+        uint32_t wb = 0u;
+        if (lane == 0 && m) wb = atomicAdd(&S.out, (uint32_t)__popcll(m));
+        wb = (uint32_t)__shfl((int)wb, 0);
+        if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
+    }
+    // crowded slots (a key repeated more than kSortMaxM times hashes there), one
+    // per wave: each round takes the first key not yet counted as the pivot, counts
+    // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
+    for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kBlk / 64) {
+        const uint32_t sl = S.hot[hs];
+        const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
+        uint32_t c = a;
+        for (;;) {
+            unsigned long long piv = kEmptyH;
+            for (; c < e; c += 64) {
+                const uint32_t q = c + (uint32_t)lane;
+                const unsigned long long x = q < e ? S.sk[q] : kEmptyH;
+                const uint64_t bal = __ballot(x != kEmptyH);
+                if (bal) {
+                    const int f = __builtin_ctzll(bal);
+                    piv = (unsigned long long)__shfl((long long)x, f);
+                    c += (uint32_t)f;
+                    break;
+                }
+            }
+            if (c >= e) break;  // wave-uniform
+            uint32_t cnt = 0u;
+            for (uint32_t q0 = c; q0 < e; q0 += 64) {
+                const uint32_t q = q0 + (uint32_t)lane;
+                const bool eq = q < e && S.sk[q] == piv;
+                cnt += (uint32_t)__popcll(__ballot(eq));
+                if (eq) S.sk[q] = kEmptyH;
+            }
+            if (lane == 0) emit_pair(p, b0 + atomicAdd(&S.out, 1u), piv, cnt);
+            ++c;
+        }
+    }
+    lds_barrier();  // E: every key emitted
+    if (tid == 0) p.ndist[l] = S.out;
+}
+
+// K4s, common instance: every list; those longer than sort_cap go to the big
+// instance (up to sort_cap_big keys) or to the table kernel.
+__global__ __launch_bounds__(SortSmall::kBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_sort_kernel(
+    HParams p) {
+    __shared__ __attribute__((aligned(16))) K4sLds<SortSmall> S;
     for (int64_t l = blockIdx.x; l < p.lists; l += gridDim.x) {
         const uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1];
         const uint32_t n = (uint32_t)(e0 - b0 < 0xFFFFFFFFull ? e0 - b0 : 0xFFFFFFFFull);
         if (n > p.sort_cap) {  // workgroup-uniform
-            if (tid == 0) defer_list(p, l, b0, e0);
+            if (threadIdx.x == 0) {
+                if (n <= p.sort_cap_big) queue_list(p.big, p.nbig, l, b0, e0);
+                else defer_list(p, l, b0, e0);
+            }
             continue;
         }
-        unsigned long long kh[kSortRes];
-#pragma unroll
-        for (int j = 0; j < kSortRes; ++j) {
-            const uint32_t i = (uint32_t)(j * kSortBlock + tid);
-            kh[j] = i < n ? p.ent[b0 + i] : kEmptyH;
-        }
-        reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
-        reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
-        lds_barrier();  // A: counters zero; the previous list is done
-        if (tid == 0) {
-            S.out = 0u;
-            S.nhot = 0u;
-        }
-        // rank: one returning add per key on its slot's 16-bit counter
-        uint32_t rk[kSortRes / 2];  // ranks (< 2^16), two per register
-#pragma unroll
-        for (int j = 0; j < kSortRes; ++j) {
-            if ((j & 1) == 0) rk[j >> 1] = 0u;
-            if ((uint32_t)(j * kSortBlock + tid) < n) {
-                const uint32_t sl = (uint32_t)kh[j] & (kSortSlots - 1);
-                const uint32_t o = __hip_atomic_fetch_add(&S.sc[sl >> 1], (sl & 1u) ? 0x10000u : 1u, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-                rk[j >> 1] |= half16(o, sl & 1u) << (16 * (j & 1));
-            }
-        }
-        lds_barrier();  // B: every key ranked
-        // scan: thread t owns counter words 8t .. 8t+7 (slots 16t .. 16t+15)
-        const uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
-        const uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
-        uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        uint32_t run = 0u;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint32_t c0 = w[i] & 0xFFFFu, c1 = w[i] >> 16;
-            if (__builtin_expect(c0 > kSortMaxM, 0)) {
-                const uint32_t x = atomicAdd(&S.nhot, 1u);
-                if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i;
-            }
-            if (__builtin_expect(c1 > kSortMaxM, 0)) {
-                const uint32_t x = atomicAdd(&S.nhot, 1u);
-                if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i + 1u;
-            }
-            w[i] = run | ((run + c0) << 16);  // exclusive starts, relative to the thread
-            run += c0 + c1;
-        }
-        uint32_t incl = run;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += y;
-        }
-        if (lane == 63) S.wsum[wv] = incl;
-        lds_barrier();  // C1: wave totals
-        uint32_t base = incl - run;
-#pragma unroll
-        for (int v = 0; v < kSortBlock / 64; ++v) base += v < wv ? S.wsum[v] : 0u;
-        const uint32_t bb = base | (base << 16);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w[i] += bb;  // starts < 2^16: no carry between the halves
-        reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
-        reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
-        lds_barrier();  // C2: slot starts
-        const uint32_t nhot = S.nhot;
-        if (nhot > kHotMax) {  // too many crowded slots: the probed table counts this list (uniform)
-            if (tid == 0) defer_list(p, l, b0, e0);
-            continue;  // (the next list's barrier A orders the LDS reuse)
-        }
-        // scatter: a key alone in its slot (the common case: ~4 K keys over 8 192
-        // slots) is a distinct key of count 1 and leaves at once; the others go to
-        // sk, and those of slots with at most kSortMaxM keys to this wave's queue
-        // of keys to check against their slot
-        uint32_t qn = 0u;  // wave-uniform
-#pragma unroll
-        for (int j = 0; j < kSortRes; ++j) {
-            bool alone = false, shared = false;
-            uint32_t pos = 0u;
-            if ((uint32_t)(j * kSortBlock + tid) < n) {
-                const uint32_t sl = (uint32_t)kh[j] & (kSortSlots - 1);
-                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
-                const uint32_t m = slot_start(S, sl + 1u, n) - a;
-                pos = a + half16(rk[j >> 1], j & 1);
-                alone = m == 1u;
-                if (!alone) {
-                    S.sk[pos] = kh[j];
-                    shared = m <= kSortMaxM;
-                }
-            }
-            const uint64_t am = __ballot(alone);
-            if (am) {
-                uint32_t wb = 0u;
-                if (lane == 0) wb = atomicAdd(&S.out, (uint32_t)__popcll(am));
-                wb = (uint32_t)__shfl((int)wb, 0);
-                if (alone) emit_pair(p, b0 + wb + (uint32_t)__popcll(am & lt), kh[j], 1u);
-            }
-            const uint64_t sm = __ballot(shared);
-            if (shared) wq[qn + (uint32_t)__popcll(sm & lt)] = (uint16_t)pos;
-            qn += (uint32_t)__popcll(sm);
-        }
-        lds_barrier();  // D: the shared keys sorted by slot
-        // the wave's queued keys, 64 at a time: the first occurrence in its slot is
-        // emitted with the slot's count of its key
-        for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
-            const bool act = q0 + (uint32_t)lane < qn;
-            bool first = false;
-            uint32_t cnt = 1u;
-            unsigned long long h = 0;
-            if (act) {
-                const uint32_t pos = wq[q0 + lane];
-                h = S.sk[pos];
-                const uint32_t sl = (uint32_t)h & (kSortSlots - 1);
-                const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
-                first = true;
-                for (uint32_t q = a; q < e; ++q) {  // 2 <= m <= kSortMaxM
-                    if (q != pos && S.sk[q] == h) {
-                        ++cnt;
-                        first = first && q > pos;
-                    }
-                }
-            }
-            const uint64_t m = __ballot(first);
-            uint32_t wb = 0u;
-            if (lane == 0 && m) wb = atomicAdd(&S.out, (uint32_t)__popcll(m));
-            wb = (uint32_t)__shfl((int)wb, 0);
-            if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
-        }
-        // crowded slots (a key repeated more than kSortMaxM times hashes there), one
-        // per wave: each round takes the first key not yet counted as the pivot, counts
-        // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
-        for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kSortBlock / 64) {
-            const uint32_t sl = S.hot[hs];
-            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
-            uint32_t c = a;
-            for (;;) {
-                unsigned long long piv = kEmptyH;
-                for (; c < e; c += 64) {
-                    const uint32_t q = c + (uint32_t)lane;
-                    const unsigned long long x = q < e ? S.sk[q] : kEmptyH;
-                    const uint64_t bal = __ballot(x != kEmptyH);
-                    if (bal) {
-                        const int f = __builtin_ctzll(bal);
-                        piv = (unsigned long long)__shfl((long long)x, f);
-                        c += (uint32_t)f;
-                        break;
-                    }
-                }
-                if (c >= e) break;  // wave-uniform
-                uint32_t cnt = 0u;
-                for (uint32_t q0 = c; q0 < e; q0 += 64) {
-                    const uint32_t q = q0 + (uint32_t)lane;
-                    const bool eq = q < e && S.sk[q] == piv;
-                    cnt += (uint32_t)__popcll(__ballot(eq));
-                    if (eq) S.sk[q] = kEmptyH;
-                }
-                if (lane == 0) emit_pair(p, b0 + atomicAdd(&S.out, 1u), piv, cnt);
-                ++c;
-            }
-        }
-        lds_barrier();  // E: every key emitted
-        if (tid == 0) p.ndist[l] = S.out;
+        sort_list<SortSmall>(p, S, l, b0, e0, n);
+    }
+}
+
+// K4s, big instance: the lists the common instance handed over (workgroups beyond
+// their number exit at once).
+__global__ __launch_bounds__(SortBig::kBlock) void canon_sort_big_kernel(HParams p) {
+    __shared__ __attribute__((aligned(16))) K4sLds<SortBig> S;
+    const int64_t nl = (int64_t)*p.nbig;
+    for (int64_t i = blockIdx.x; i < nl; i += gridDim.x) {
+        const uint64_t b0 = p.big[3 * i + 1], e0 = p.big[3 * i + 2];
+        sort_list<SortBig>(p, S, (int64_t)p.big[3 * i], b0, e0, (uint32_t)(e0 - b0));
     }
 }
 
@@ -1164,6 +1213,7 @@ std::mutex h_mu;
 std::vector<HCache> h_ws;
 uint32_t h_claim_cap = kClaimW;
 uint32_t h_sort_cap = kSortCap;
+uint32_t h_sort_cap_big = kSortCapBig;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1187,6 +1237,7 @@ extern "C" KMC_DIAG_API int kmc_diag_canon_claim_cap(unsigned cap) {
 extern "C" KMC_DIAG_API int kmc_diag_canon_sort_cap(unsigned cap) {
     std::lock_guard<std::mutex> lk(h_mu);
     h_sort_cap = cap > kSortCap ? kSortCap : cap;
+    h_sort_cap_big = cap == 0 ? 0u : kSortCapBig;  // 0: no counting sort at all (every list to the table)
     return KMC_OK;
 }
 #endif
@@ -1204,7 +1255,7 @@ struct CanonPlan {
     std::vector<int2> fsplit;
     int64_t M = 0, Mc = 0, L = 0, windows = 0;
     size_t o_idx, o_lg, o_cb, o_ccb, o_w0, o_nw, o_lb, o_fs, o_cnt, o_off, o_cntc, o_offc, o_bs, o_ent, o_ls, o_pk,
-        o_pc, o_nd, o_do, o_err, o_dn, o_dl, total;
+        o_pc, o_nd, o_do, o_err, o_dn, o_dl, o_bn, o_bl, total;
 };
 
 void canon_plan(const int64_t *hidx, int64_t n, int k, int cus, CanonPlan &P) {
@@ -1274,6 +1325,8 @@ void canon_plan(const int64_t *hidx, int64_t n, int k, int cus, CanonPlan &P) {
     P.o_err = o; o += al256(4);
     P.o_dn = o; o += al256(8);
     P.o_dl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
+    P.o_bn = o; o += al256(8);
+    P.o_bl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
     P.total = o;
 }
 
@@ -1286,11 +1339,11 @@ int device_cus(int device, int *cus) {
 extern "C" size_t kmc_count_canonical_workspace_size(const int64_t *host_indices, uint64_t num_seqs, int k,
                                                     int device) {
     if (!host_indices || k < 1 || k > KMC_CANON_MAX_K || num_seqs == 0) return 0;
-    int cus = 0;
-    if (device_cus(device, &cus)) return 0;
     const int64_t n = (int64_t)num_seqs;
     for (int64_t r = 0; r < n; ++r)
         if (host_indices[r + 1] < host_indices[r]) return 0;
+    int cus = 0;  // (the arguments are checked before any HIP call)
+    if (device_cus(device, &cus)) return 0;
     // the size for every alignment of `data` (a misaligned pointer shifts the offsets
     // by up to 15 bytes, which can move a record's chunks to another workgroup)
     std::vector<int64_t> b(n + 1);
@@ -1402,6 +1455,9 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     p.err = reinterpret_cast<uint32_t *>(ws + o_err);
     p.claim_cap = h_claim_cap;
     p.sort_cap = h_sort_cap;
+    p.sort_cap_big = h_sort_cap_big;
+    p.nbig = reinterpret_cast<unsigned long long *>(ws + P.o_bn);
+    p.big = reinterpret_cast<uint64_t *>(ws + P.o_bl);
     p.ndefer = reinterpret_cast<unsigned long long *>(ws + o_dn);
     p.defer = reinterpret_cast<uint64_t *>(ws + o_dl);
     p.rec_off = rec_offsets;
@@ -1417,7 +1473,9 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
         (NF && (he = hipMemcpyAsync((void *)p.fsplit, fsplit.data(), NF * sizeof(int2), hipMemcpyHostToDevice,
                                     stream))))
         return (int)he;
-    if ((he = hipMemsetAsync(p.err, 0, 4, stream)) || (he = hipMemsetAsync(p.ndefer, 0, 8, stream))) return (int)he;
+    if ((he = hipMemsetAsync(p.err, 0, 4, stream)) || (he = hipMemsetAsync(p.ndefer, 0, 8, stream)) ||
+        (he = hipMemsetAsync(p.nbig, 0, 8, stream)))
+        return (int)he;
     if (M > 0) {
         if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream)) ||
             (he = hipMemsetAsync(p.cnt_c, 0, (size_t)Mc * 4, stream)))
@@ -1432,6 +1490,11 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     // persistent, two workgroups per CU (64 KB of LDS each), striding over the lists
     hipLaunchKernelGGL(canon_sort_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 2 * (int64_t)cus))),
                        dim3(kSortBlock), 0, stream, p);
+    // the lists it handed to its big instance (one 1 024-thread workgroup per CU;
+    // workgroups beyond their number exit at once), before the table kernel, which
+    // also takes the big instance's deferrals
+    hipLaunchKernelGGL(canon_sort_big_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (int64_t)cus))),
+                       dim3(SortBig::kBlock), 0, stream, p);
     // the deferred lists (count on the device): two workgroups per CU (their tables
     // fill the LDS) striding over them; workgroups beyond the count exit at once
     hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (1024 / kCountBlock) * (int64_t)cus))),

@@ -60,6 +60,24 @@
 #ifndef KMC_RING_RT
 #define KMC_RING_RT 1
 #endif
+// R3 ring addressing when a ring is 64 entries (k = 13): 1 = circular (list index
+// g in slot (g mod 64) ^ swz, so the partial last segment stays in place: no tail
+// move in the flush), 0 = rebased every round (the partial segment copied to the
+// ring's start)
+#ifndef KMC_RING_CIRC
+#define KMC_RING_CIRC 0
+#endif
+// R3 flush: 1 = a quad reads a segment's chunks only when it stores one (reads
+// predicated), 0 = unconditional reads
+#ifndef KMC_FLUSH_PRED
+#define KMC_FLUSH_PRED 0
+#endif
+// R4 list end: 1 = one pass over the LDS bins that writes the stage row, sums the
+// bins (wrap check) and clears them for the next list; 0 = a sum pass, a write
+// pass and a clear pass
+#ifndef KMC_R4_FUSE
+#define KMC_R4_FUSE 0
+#endif
 
 namespace kmc {
 namespace {
@@ -323,6 +341,17 @@ __device__ __forceinline__ uint32_t ring_word(uint32_t b, uint32_t f0) {
     return ((b * (uint32_t)RingGeom<K>::RING | ring_swz(b)) << 16) | (f0 << 1);
 }
 
+// circular ring (KMC_RING_CIRC, RING = 64): the round's entries start at list index
+// f (relative to the piece's 32-aligned base); its first segment h = f & ~31 lives
+// in ring half (h & 32), which is folded into the swizzle: with x = (f & 31) + rank
+// < 64, (h + x) mod 64 = x ^ (h & 32)
+template <int K>
+__device__ __forceinline__ uint32_t ring_word_circ(uint32_t b, uint32_t f) {
+    return ((b * (uint32_t)RingGeom<K>::RING | (ring_swz(b) ^ (f & 32u))) << 16) | ((f & 31u) << 1);
+}
+template <int K>
+constexpr bool ring_circ() { return KMC_RING_CIRC && RingGeom<K>::RING == 64; }
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
@@ -432,6 +461,7 @@ struct RRingOp {
 
     // entry at relative list index g of bucket b, from the ring (h: ring slot 0's index)
     __device__ __forceinline__ uint16_t ring_entry(uint32_t b, uint32_t h, uint32_t g) const {
+        if constexpr (ring_circ<K>()) return ring[b * RG::RING + ((g & (RG::RING - 1)) ^ ring_swz(b))];
         return ring[b * RG::RING + ((g - h) ^ ring_swz(b))];
     }
 
@@ -443,7 +473,7 @@ struct RRingOp {
         f = v = f0 = (uint32_t)(F - P0);
         cap = SAMPLED ? f0 + capb : ~0u;
         if (owner) {
-            W[b] = ring_word<K>(b, f);
+            W[b] = ring_circ<K>() ? ring_word_circ<K>(b, f) : ring_word<K>(b, f);
             gH[b] = P0;
             if (SAMPLED) lim[b] = P0 + cap;
         }
@@ -468,11 +498,15 @@ struct RRingOp {
         // nseg); its chunks are read now, their latency hidden
         // (unconditional reads, inside the bucket's own ring: predicated ones
         // would each wait for the last)
-        const uint32_t nq = (fill <= (uint32_t)RG::RING && j == 0 && nseg > 0) ? ((fill & 31u) + 7u) >> 3 : 0u;
-        const uint4 tl0 = row[((4 * nseg + 0) ^ x8) & (RG::RING / 8 - 1)];
-        const uint4 tl1 = row[((4 * nseg + 1) ^ x8) & (RG::RING / 8 - 1)];
-        const uint4 tl2 = row[((4 * nseg + 2) ^ x8) & (RG::RING / 8 - 1)];
-        const uint4 tl3 = row[((4 * nseg + 3) ^ x8) & (RG::RING / 8 - 1)];
+        constexpr bool CIRC = ring_circ<K>();
+        const uint32_t nq = (!CIRC && fill <= (uint32_t)RG::RING && j == 0 && nseg > 0) ? ((fill & 31u) + 7u) >> 3 : 0u;
+        uint4 tl0, tl1, tl2, tl3;
+        if constexpr (!CIRC) {
+            tl0 = row[((4 * nseg + 0) ^ x8) & (RG::RING / 8 - 1)];
+            tl1 = row[((4 * nseg + 1) ^ x8) & (RG::RING / 8 - 1)];
+            tl2 = row[((4 * nseg + 2) ^ x8) & (RG::RING / 8 - 1)];
+            tl3 = row[((4 * nseg + 3) ^ x8) & (RG::RING / 8 - 1)];
+        }
         uint32_t i0 = j;
         if (h < v && j == 0 && nseg > 0) {  // segment 0 partly before v (piece start, after an overflow)
             for (uint32_t q = 0; q < 32; ++q)
@@ -490,13 +524,21 @@ struct RRingOp {
             // bit 2: a segment to store, bit 3: one past its region (to the overflow
             // list); bits 0-1: the chunk swizzle
             const bool in = !SAMPLED || h + 32u * i + 32u <= cap;
-            const uint32_t A = (rowb + 64u * (i ^ (x8 >> 2))) | (x8 & 3u) | (i < nseg ? (in ? 4u : 8u) : 0u);
+            // the ring half of segment i (circular: it follows the list index)
+            const uint32_t half = CIRC ? (((h >> 5) + i) & 1u) ^ (x8 >> 2) : (i ^ (x8 >> 2));
+            const uint32_t A = (rowb + 64u * half) | (x8 & 3u) | (i < nseg ? (in ? 4u : 8u) : 0u);
             uint32_t a[4], g[4];
             quad_bcast4(A, a);
             quad_bcast4(gs + i, g);
             u32x4 val[4];  // (a quad without a segment reads a chunk of its own ring harmlessly)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
+            for (int t = 0; t < 4; ++t) {
+                if (KMC_FLUSH_PRED && !(a[t] & 12u)) {
+                    val[t] = u32x4{0u, 0u, 0u, 0u};
+                } else {
+                    val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
+                }
+            }
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (a[t] & 4u) reinterpret_cast<u32x4 *>(ent + 32ull * g[t])[q] = val[t];
@@ -507,7 +549,7 @@ struct RRingOp {
         }
         if (fill > (uint32_t)RG::RING) {
             v = f1;  // [h + RING, f1) went straight to the list
-        } else {     // the partial last segment to the ring's start
+        } else if constexpr (!CIRC) {  // the partial last segment to the ring's start
             if (nq > 0) row[0 ^ x8] = tl0;
             if (nq > 1) row[1 ^ x8] = tl1;
             if (nq > 2) row[2 ^ x8] = tl2;
@@ -515,7 +557,7 @@ struct RRingOp {
         }
         f = f1;
         if (j == 0) {
-            W[(par ^ 1u) * RG::NBK + b] = ring_word<K>(b, f1 & 31u);
+            W[(par ^ 1u) * RG::NBK + b] = CIRC ? ring_word_circ<K>(b, f1) : ring_word<K>(b, f1 & 31u);
             gH[b] = P0 + (f1 & ~31u);
         }
         par ^= 1u;
@@ -818,9 +860,11 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
         }
     };
     fetch(blockIdx.x);
+    bool dirty = true;  // (KMC_R4_FUSE: the list-end pass leaves the bins cleared)
     for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
         const int64_t s = list / p.nbk, b = list % p.nbk;
-        for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
+        if (!KMC_R4_FUSE || dirty)
+            for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         if (threadIdx.x == 0) s_sum = 0ull;
         uint64_t beg, end;  // entries of the list (REG: beg = 0, end = their number)
         const int nreg = p.G;
@@ -856,7 +900,30 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
         }
         __syncthreads();
         uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
-        if constexpr (LOW <= 15) {
+        if constexpr (KMC_R4_FUSE) {
+            // one pass: stage row written, bins summed (LOW = 16: wrap check) and cleared
+            uint32_t part = 0u;
+            for (int i = threadIdx.x; i < kWords; i += 1024) {
+                const uint32_t w = h[i];
+                h[i] = 0u;
+                if constexpr (LOW <= 15) {
+                    dst[i] = w;
+                } else {
+                    part += (w & 0xFFFFu) + (w >> 16);
+                    reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
+                }
+            }
+            dirty = false;
+            if constexpr (LOW > 15) {
+                atomicAdd(&s_sum, (unsigned long long)part);
+                __syncthreads();
+                if (s_sum != end - beg) {  // a bin wrapped: the exact recount overwrites the row
+                    if constexpr (REG) hist_recount_regions<LOW>(p.ent, s_rb, s_rn, nreg, h, dst);
+                    else hist_recount<LOW>(p.ent, beg, end, h, dst);
+                    dirty = true;
+                }
+            }
+        } else if constexpr (LOW <= 15) {
             for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
         } else {
             uint32_t part = 0u;

@@ -105,6 +105,7 @@ def _load(path):
     L.kmc_error_string.restype = ctypes.c_char_p
     L.kmc_error_string.argtypes = [ctypes.c_int]
     L.kmc_version.restype = ctypes.c_int
+    L.kmc_version.argtypes = []
     L.sumKmereCoincidencesGlobalMemory_hip.argtypes = [_P, _P, ctypes.c_uint, _P, _P]
     L.kmc_count_dense_workspace_size.restype = ctypes.c_size_t
     L.kmc_count_dense_workspace_size.argtypes = [ctypes.c_int, _U64, _U64, ctypes.c_int]
@@ -142,6 +143,10 @@ def _load(path):
     L.minKmeres2_hip.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P, _P]
     L.kmc_count_canonical_hash.argtypes = [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _P, _P, _U64, _P,
                                            ctypes.POINTER(_U64), _P]
+    L.kmc_count_canonical_hash_ex.argtypes = [_P, _P, _U64, ctypes.c_int, ctypes.c_uint, _P, _P, _U64, _P,
+                                              ctypes.POINTER(_U64), _P, ctypes.c_size_t, _P]
+    L.kmc_count_canonical_workspace_size.restype = ctypes.c_size_t
+    L.kmc_count_canonical_workspace_size.argtypes = [_P, _U64, ctypes.c_int, ctypes.c_int]
     return L
 
 

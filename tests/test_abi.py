@@ -14,6 +14,13 @@ def test_library_exports_every_header_symbol(kmc):
     assert not missing, missing
 
 
+def test_binding_declares_every_signature(kmc):
+    """kmc.py sets argtypes for every entry point of the header (ctypes would
+    otherwise pass Python ints as 32-bit ints: 64-bit sizes silently truncated)."""
+    L = kmc.lib()
+    assert [n for n in kmc.header_symbols() if getattr(L, n).argtypes is None] == []
+
+
 def _dynamic_symbols(path):
     out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
     return sorted(l.split()[-1] for l in out.splitlines() if l.strip())

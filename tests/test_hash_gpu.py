@@ -195,6 +195,46 @@ def test_canonical_size_independent_properties(kmc, cuda):
     assert np.all(kk <= rc)
 
 
+def test_canonical_big_lists_sort_vs_table(kmc, cuda):
+    """A chromosome-sized record (240 Mbase: 2^15 lists of ~7.3 K keys, above the
+    common K4s instance's 6 080) is counted by the big K4s instance; its (key, count)
+    set equals the probed table kernel's (every list forced there through the
+    diagnostic library), and its counts sum to the windows.  A 60 Mbase record with
+    a 3 Mbase tandem repeat beside it crowds slots of its lists (deferred)."""
+    import torch
+    L = 240_000_000
+    A = (L + 1 + 15) & ~15  # record 2's synthetic bases start 16-aligned (synth_fill), after N padding
+    data = torch.empty(A + 60_000_001 + 16, dtype=torch.uint8, device=cuda)
+    kmc.synth_fill(data, 1, L, 0x5EED0B16)
+    data[L + 1:A] = ord("N")
+    kmc.synth_fill(data[A:], 1, 60_000_000, 0x5EED0B17)
+    unit = torch.from_numpy(np.frombuffer(b"ACGTTGCATTAGCCAGT" * 3, dtype=np.uint8).copy()).to(cuda)
+    rep = unit.repeat(3_000_000 // unit.numel() + 1)[:3_000_000]
+    data[A + 1000:A + 1000 + rep.numel()] = rep
+    idx = np.array([0, L + 1, A + 60_000_001], dtype=np.int64)
+    di = dev(idx, cuda)
+
+    def run(k):
+        keys, counts, off = kmc.count_canonical(data, di, k, capacity=L + 60_000_000)
+        torch.cuda.synchronize()
+        out = []
+        for s in range(2):
+            a, b = int(off[s]), int(off[s + 1])
+            o = torch.argsort(keys[a:b])
+            out.append((keys[a:b][o], counts[a:b][o]))
+        return out
+
+    for k in (31, 25):
+        got = run(k)
+        with kmc.diag() as D:
+            assert D.kmc_diag_canon_sort_cap(0) == 0
+            ref = run(k)
+        for s, ((gk, gc), (rk, rc)) in enumerate(zip(got, ref)):
+            assert torch.equal(gk, rk) and torch.equal(gc, rc), "k=%d record %d" % (k, s)
+        assert int(got[0][1].to(torch.int64).sum()) == L - k + 1
+        assert int(got[1][1].to(torch.int64).sum()) == 60_000_000 - k + 1
+
+
 def test_canonical_capacity_error(kmc, cuda):
     import torch
     rng = np.random.default_rng(1)
@@ -234,7 +274,7 @@ def test_canonical_unaligned_data_and_caller_workspace(kmc, oracle, cuda, k):
     """The canonical entry point takes any data pointer (rounded down to 16 bytes,
     offsets biased, as the dense path does): data + 1, 7, 8, 15 of a buffer give the
     self-oracle's counts; kmc_count_canonical_hash_ex with a caller workspace of the
-    queried size gives the same, and a workspace one byte short is refused."""
+    queried size gives the same, and half that workspace is refused."""
     import torch
     rng = np.random.default_rng(900 + k)
     data, idx = random_records(rng, [0, 5, 40_000, 1, 333_333, 64], b"ACGTNacgt",
@@ -257,6 +297,14 @@ def test_canonical_unaligned_data_and_caller_workspace(kmc, oracle, cuda, k):
         torch.cuda.synchronize()
         got = (keys.cpu().numpy().view(np.uint64), counts.cpu().numpy().view(np.uint32), ro.cpu().numpy())
         assert_same(got, exp, "caller workspace, offset %d" % off)
-    with pytest.raises(kmc.KmcError) as e:
-        kmc.count_canonical(d, di, k, flags=kmc.CANON_SOFTMASK, capacity=data.size, workspace=ws[:wsb - 1])
-    assert e.value.code == 1004
+    # ~20 B per window plus per-list tables (the size holds for every alignment)
+    assert 16 * 373_367 < wsb < 32 * 373_367 + (1 << 20), wsb
+    refused = []
+    for frac in (2, 4, 8, 64):
+        try:
+            kmc.count_canonical(d, di, k, flags=kmc.CANON_SOFTMASK, capacity=data.size, workspace=ws[:wsb // frac])
+            torch.cuda.synchronize()
+        except kmc.KmcError as e:
+            assert e.code == 1004
+            refused.append(frac)
+    assert refused and refused[-1] == 64, (wsb, refused)
