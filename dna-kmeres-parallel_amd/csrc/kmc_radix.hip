@@ -63,20 +63,18 @@
 // R3 ring addressing when a ring is 64 entries (k = 13): 1 = circular (list index
 // g in slot (g mod 64) ^ swz, so the partial last segment stays in place: no tail
 // move in the flush), 0 = rebased every round (the partial segment copied to the
-// ring's start)
+// ring's start).  Round 4, same box (profiles/r04b_r3_variants.txt): R3 8.78-8.83
+// -> 8.34-8.40 ms, C3 14.59-14.65 -> 14.14-14.18 ms.  (Reading a segment's chunks
+// only when the quad stores one, instead of unconditionally, made R3 24 ms: the
+// flush is latency-bound, and the predicated reads serialised it.)
 #ifndef KMC_RING_CIRC
-#define KMC_RING_CIRC 0
-#endif
-// R3 flush: 1 = a quad reads a segment's chunks only when it stores one (reads
-// predicated), 0 = unconditional reads
-#ifndef KMC_FLUSH_PRED
-#define KMC_FLUSH_PRED 0
+#define KMC_RING_CIRC 1
 #endif
 // R4 list end: 1 = one pass over the LDS bins that writes the stage row, sums the
 // bins (wrap check) and clears them for the next list; 0 = a sum pass, a write
-// pass and a clear pass
+// pass and a clear pass.  Round 4, same box: R4 4.34 -> 4.19 ms.
 #ifndef KMC_R4_FUSE
-#define KMC_R4_FUSE 0
+#define KMC_R4_FUSE 1
 #endif
 
 namespace kmc {
@@ -532,13 +530,7 @@ struct RRingOp {
             quad_bcast4(gs + i, g);
             u32x4 val[4];  // (a quad without a segment reads a chunk of its own ring harmlessly)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (KMC_FLUSH_PRED && !(a[t] & 12u)) {
-                    val[t] = u32x4{0u, 0u, 0u, 0u};
-                } else {
-                    val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
-                }
-            }
+            for (int t = 0; t < 4; ++t) val[t] = *(const lds_u32x4 *)(uintptr_t)((a[t] & ~63u) + 16u * (q ^ (a[t] & 3u)));
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (a[t] & 4u) reinterpret_cast<u32x4 *>(ent + 32ull * g[t])[q] = val[t];
