@@ -64,6 +64,18 @@
 #ifndef KMC_FINE_PF
 #define KMC_FINE_PF 1
 #endif
+// K3b: wait for those loads before the round's flush issues its segment stores (gfx9
+// counts stores in vmcnt: the compiler's wait for the prefetched entries at the loop
+// bottom otherwise also waits for every store of the flush; the radix R3's
+// KMC_R3_PREWAIT is the same change)
+#ifndef KMC_K3B_PREWAIT
+#define KMC_K3B_PREWAIT 0
+#endif
+// K3a: the same before the staged round's run stores (the next round's chunk was
+// loaded at the top of the iteration, before the current one was hashed)
+#ifndef KMC_K3A_PREWAIT
+#define KMC_K3A_PREWAIT 0
+#endif
 
 namespace kmc {
 namespace {
@@ -212,11 +224,33 @@ __device__ __forceinline__ void chunk_codes(uint4 r, bool soft, uint32_t &code, 
 struct ChunkRaw {
     uint4 r[3];
 };
+// Round 4: three unconditional raw buffer loads over [the wave's first chunk, the
+// end of the last record rounded up to 16 bytes): the hardware range check returns
+// zeros past it, so no lane branches around its loads.  (load16's per-lane bounds
+// branch made the compiler wait for the prefetched chunk -- s_waitcnt vmcnt(0) at
+// the bottom of every iteration -- so the walks had one chunk in flight per thread
+// and paid the full HBM latency per round.)  Bytes between the last record's end
+// and the next 16-byte boundary are read but never reach a counted window (every
+// counted window ends before its record's terminator), and that block never
+// crosses a page.  q is 16-aligned; the wave's lane 0 holds its smallest q.
 __device__ __forceinline__ ChunkRaw chunk_raw(const HParams &p, int64_t q) {
-    const int64_t hi_byte = p.idx[p.n];
+    const int64_t hi16 = (p.hi + 15) & ~(int64_t)15;  // p.hi = idx[n] (a kernel argument: no load)
+    // (both halves zero-extended: a sign-extended low half would corrupt q >= 2^31)
+    const int64_t base = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)q) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)q >> 32))
+                                    << 32));
+    int64_t nrec = hi16 - base;
+    nrec = nrec < 0 ? 0 : (nrec > (1ll << 31) ? (1ll << 31) : nrec);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(p.data) + base, (short)0, (int)nrec, 0x00020000);
+    const int off = (int)(q - base);
     ChunkRaw c;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int i = 0; i < 3; ++i) c.r[i] = load16(p.data, q + 16 * i, hi_byte);
+    for (int i = 0; i < 3; ++i) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * i, 0, 0);
+        c.r[i] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
     return c;
 }
 
@@ -242,12 +276,24 @@ __device__ __forceinline__ uint32_t chunk_keys(const HParams &p, const ChunkRaw 
     // the MSB-first key of window 0 by bit reversal, then rolled one base per
     // window: base j + k - 1 enters at the low end, read from t = the chunk's
     // codes from base k - 1 on (2 <= 2(k - 1) <= 60)
+    // windows holding an invalid base: bit j of the smeared mask = OR of badm's bits
+    // j .. j+k-1 (log2 k wave-uniform doubling steps per chunk, instead of a 64-bit
+    // shift, mask and compare per window)
+    {
+        uint64_t sm = badm;
+        for (int c = 1; c < k;) {
+            const int st = c < k - c ? c : k - c;
+            sm |= sm >> st;
+            c += st;
+        }
+        vm &= ~(uint32_t)sm;
+    }
+    (void)wmask;
     uint64_t fw = reverse_groups(lo64 & kmask, k);
     const int sk = 2 * (k - 1);
     const uint64_t t = sk == 0 ? lo64 : (lo64 >> sk) | ((uint64_t)cd[2] << (64 - sk));
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        if ((badm >> j) & wmask) vm &= ~(1u << j);
         const uint64_t le = (j == 0 ? lo64 : ((lo64 >> (2 * j)) | ((uint64_t)cd[2] << (64 - 2 * j)))) & kmask;
         if (j > 0) fw = ((fw << 2) | ((t >> (2 * j)) & 3u)) & kmask;
         h[j] = part_of(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
@@ -296,11 +342,11 @@ __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
         const int64_t qs = (int64_t)kWalkBlock << 4;
         int64_t q = ((ps >> 4) + threadIdx.x) << 4;
         ChunkRaw nx;
-        if (KMC_WALK_PF && q < pe) nx = chunk_raw(p, q);
+        if (KMC_WALK_PF) nx = chunk_raw(p, q);  // (unconditional: past the piece it reads harmlessly)
         for (; q < pe; q += qs) {
             unsigned long long h[16];
             const ChunkRaw cr = KMC_WALK_PF ? nx : chunk_raw(p, q);
-            if (KMC_WALK_PF && q + qs < pe) nx = chunk_raw(p, q + qs);  // the next chunk, in flight
+            if (KMC_WALK_PF) nx = chunk_raw(p, q + qs);  // the next chunk, in flight
             const uint32_t vm = chunk_keys(p, cr, q, ps, pe, rend, h);
 #pragma unroll
             for (int j = 0; j < 16; ++j)
@@ -557,15 +603,20 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
         const auto bk = [lgc](unsigned long long x) { return lgc ? (uint32_t)(x >> (64 - lgc)) : 0u; };
         const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
         ChunkRaw nx;
-        if (KMC_WALK_PF && c0 + threadIdx.x < c1) nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
+        if (KMC_WALK_PF) nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
+        // (K3A_PREWAIT: the first chunk waited for here too, so that nothing is left
+        // pending on either path into the loop and its top needs no wait -- which
+        // would also wait for the previous round's stores)
+        if (KMC_K3A_PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);
         for (int64_t cb = c0; cb < c1; cb += kWalkBlock) {
             const int64_t c = cb + threadIdx.x;
             unsigned long long h[16];
             uint32_t vm = 0u;
             ChunkRaw cr = nx;
             if (!KMC_WALK_PF && c < c1) cr = chunk_raw(p, c << 4);
-            if (KMC_WALK_PF && c + kWalkBlock < c1) nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
+            if (KMC_WALK_PF) nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
             if (c < c1) vm = chunk_keys(p, cr, c << 4, ps, pe, rend, h);
+            if (KMC_K3A_PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
             if (lg > lgc)
                 staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return x; }, dst);
             else  // buckets are the lists
@@ -635,6 +686,7 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
             v[j] = list_value(x[j]);
         }
         rg.add<8>(v, bk, vm);
+        if (KMC_K3B_PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
         rg.round_end();
     }
     rg.finish();

@@ -1,4 +1,4 @@
-# GPU (round 4): R3 flush variants of the radix path (scripts/build_radix_variants.sh:
+# GPU (round 4): R3 flush variants of the radix path (scripts/build_src_variants.sh:
 # base, circular ring, predicated flush reads, both), timed same-box in alternating
 # order on C3's 10 Gbase k = 13 pipeline (kbench under rocprofv3 kernel trace),
 # then the radix parity tests on the variant VARIANT_TEST (KMC_LIB + KMC_DIAG_LIB),

@@ -4,7 +4,7 @@
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/r04c && mkdir -p $O && rm -rf $O/*
 run() { local t=$1; shift; timeout -k 10 $t "$@"; local rc=$?; if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*"; exit $rc; fi; }
 if [ -n "$TESTS" ]; then
-  run 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu tests/test_dense_gpu.py tests/test_baseline_configs_gpu.py -k "$TESTS" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+  run 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu ${TFILES:-tests/test_dense_gpu.py tests/test_baseline_configs_gpu.py} -k "$TESTS" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
   tail -1 $O/tests.log
 fi
 run 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/cb -o cb -- python3 scripts/cbench.py --iters 3 --configs ${CB:-c3,c4,c4r} > $O/cb.log 2>&1

@@ -308,3 +308,24 @@ def test_canonical_unaligned_data_and_caller_workspace(kmc, oracle, cuda, k):
             assert e.code == 1004
             refused.append(frac)
     assert refused and refused[-1] == 64, (wsb, refused)
+
+
+@pytest.mark.parametrize("k", [31, 17])
+def test_canonical_offsets_beyond_2gib(kmc, oracle, cuda, k):
+    """Records that lie past byte 2^31 of the buffer (the C4 genome is 3.1 GB): the
+    input walks address their chunks through 64-bit wave bases (a sign-extended
+    32-bit half once dropped every window there), counts equal the self-oracle's."""
+    import torch
+    rng = np.random.default_rng(2031 + k)
+    data, idx = random_records(rng, [3_000_000, 1, 1_000_001], b"ACGTNacgt",
+                               (.2, .2, .2, .2, .04, .04, .04, .04, .04))
+    base = (1 << 31) + 4096 + 7
+    buf = torch.empty(base + data.size + 64, dtype=torch.uint8, device=cuda)
+    buf[base:base + data.size] = dev(data, cuda)
+    gidx = dev(idx + base, cuda)
+    keys, counts, off = kmc.count_canonical(buf, gidx, k, flags=kmc.CANON_SOFTMASK, capacity=data.size)
+    torch.cuda.synchronize()
+    got = (keys.cpu().numpy().view(np.uint64), counts.cpu().numpy().view(np.uint32), off.cpu().numpy())
+    assert_same(got, oracle.count_canonical(data, idx, k, soft=True), "k=%d" % k)
+    del buf
+    torch.cuda.empty_cache()
