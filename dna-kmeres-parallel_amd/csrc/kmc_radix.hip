@@ -76,15 +76,6 @@
 #ifndef KMC_R4_FUSE
 #define KMC_R4_FUSE 1
 #endif
-// R3: wait for the prefetched tiles (all but the newest KMC_RSCAT_PF - 2) before the
-// flush issues its segment stores.  On gfx9 vmcnt counts stores with loads, and the
-// flush's store count is data-dependent, so the compiler's wait for the next tile
-// at the top of the next step (vmcnt(PF - 1)) also waited for every store of the
-// flush to be acknowledged; waiting here, where the tile has long arrived, lets the
-// stores drain behind the next round's ranking.
-#ifndef KMC_R3_PREWAIT
-#define KMC_R3_PREWAIT 0
-#endif
 
 namespace kmc {
 namespace {
@@ -567,10 +558,6 @@ struct RRingOp {
     __device__ void after_iter(int64_t i, int64_t per, bool) {
         if (++held < KMC_RING_RT && i + 1 < per) return;
         held = 0;
-        if constexpr (KMC_R3_PREWAIT) {
-            static_assert(KMC_RSCAT_PF >= 2 && KMC_RSCAT_PF <= 17, "vmcnt encoding");
-            __builtin_amdgcn_s_waitcnt(0x0F70 | (KMC_RSCAT_PF - 2));  // vmcnt(PF - 2), gfx9 encoding
-        }
         lds_barrier();  // every window of the round is ranked and in its ring
         flush();
         lds_barrier();  // rings read, W set up: the next round may write
