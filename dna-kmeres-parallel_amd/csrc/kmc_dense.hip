@@ -42,6 +42,13 @@
 
 // k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
 // spill entries (0: no scans)
+// Round 4: the workgroup's first record found by one load per thread (n <= BLOCK)
+// instead of a binary search by one thread, the LDS histogram cleared and the
+// slab flush done 16 bytes per lane (the fixed part of a launch, which an 8-way
+// shard's step pays on 1/8 of the work)
+#ifndef KMC_DENSE_VEC
+#define KMC_DENSE_VEC 1
+#endif
 #ifndef KMC_HM3_SCAN
 #define KMC_HM3_SCAN 256
 #endif
@@ -310,26 +317,42 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     if (tb < te) {
         const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
         const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
-        if (tid == 0) {
-            // last record s with indices[s] <= R0 (records before it end before R0)
-            int64_t lo = 0, hi = p.n - 1;
-            if (rec_off<Idx>(p, 0) <= R0) {
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi + 1) >> 1;
-                    if (rec_off<Idx>(p, mid) <= R0) lo = mid;
-                    else hi = mid - 1;
-                }
+        int64_t s0 = 0;
+        if (KMC_DENSE_VEC && p.n <= BLOCK) {
+            // last record s with indices[s] <= R0 (records before it end before R0;
+            // the offsets are sorted): the number of such records, less one
+            if (tid == 0) {
+                misc[0] = 0u;
+                misc[3] = 0u;
+                misc[4] = 0u;
+                misc[5] = 0u;
             }
-            misc[0] = 0u;
-            misc[3] = 0u;
-            misc[4] = 0u;
-            misc[5] = 0u;
-            misc[1] = (uint32_t)lo;
-            misc[2] = (uint32_t)((uint64_t)lo >> 32);
+            const bool le = tid < p.n && rec_off<Idx>(p, tid) <= R0;
+            for (int i = tid; i < NW / 4; i += BLOCK) reinterpret_cast<uint4 *>(h)[i] = make_uint4(0u, 0u, 0u, 0u);
+            const int cnt = __syncthreads_count(le);
+            s0 = cnt > 0 ? cnt - 1 : 0;
+        } else {
+            if (tid == 0) {
+                // last record s with indices[s] <= R0 (records before it end before R0)
+                int64_t lo = 0, hi = p.n - 1;
+                if (rec_off<Idx>(p, 0) <= R0) {
+                    while (lo < hi) {
+                        const int64_t mid = (lo + hi + 1) >> 1;
+                        if (rec_off<Idx>(p, mid) <= R0) lo = mid;
+                        else hi = mid - 1;
+                    }
+                }
+                misc[0] = 0u;
+                misc[3] = 0u;
+                misc[4] = 0u;
+                misc[5] = 0u;
+                misc[1] = (uint32_t)lo;
+                misc[2] = (uint32_t)((uint64_t)lo >> 32);
+            }
+            for (int i = tid; i < NW; i += BLOCK) h[i] = 0u;
+            __syncthreads();
+            s0 = (int64_t)((uint64_t)misc[1] | ((uint64_t)misc[2] << 32));
         }
-        for (int i = tid; i < NW; i += BLOCK) h[i] = 0u;
-        __syncthreads();
-        const int64_t s0 = (int64_t)((uint64_t)misc[1] | ((uint64_t)misc[2] << 32));
 
         P16Ctx pc;
         pc.h = h;
@@ -373,6 +396,16 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 // LDS: the halves are exact, wraps live in spills); the LDS cleared
                 const auto flush = [&]() {
                     uint32_t dsum = 0u;
+                    if (KMC_DENSE_VEC && !entire) {  // the slab: 16 bytes per lane
+                        for (int i = tid; i < NW / 4; i += BLOCK) {
+                            const uint4 v = reinterpret_cast<const uint4 *>(h)[i];
+                            reinterpret_cast<uint4 *>(h)[i] = make_uint4(0u, 0u, 0u, 0u);
+                            dsum += (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) +
+                                    (v.z >> 16) + (v.w & 0xFFFFu) + (v.w >> 16);
+                            reinterpret_cast<uint4 *>(dst)[i] = v;
+                        }
+                        return dsum;
+                    }
                     for (int i = tid; i < NW; i += BLOCK) {
                         const uint32_t v = h[i];
                         h[i] = 0u;

@@ -64,18 +64,6 @@
 #ifndef KMC_FINE_PF
 #define KMC_FINE_PF 1
 #endif
-// K3b: wait for those loads before the round's flush issues its segment stores (gfx9
-// counts stores in vmcnt: the compiler's wait for the prefetched entries at the loop
-// bottom otherwise also waits for every store of the flush; the radix R3's
-// KMC_R3_PREWAIT is the same change)
-#ifndef KMC_K3B_PREWAIT
-#define KMC_K3B_PREWAIT 0
-#endif
-// K3a: the same before the staged round's run stores (the next round's chunk was
-// loaded at the top of the iteration, before the current one was hashed)
-#ifndef KMC_K3A_PREWAIT
-#define KMC_K3A_PREWAIT 0
-#endif
 
 namespace kmc {
 namespace {
@@ -254,17 +242,24 @@ __device__ __forceinline__ ChunkRaw chunk_raw(const HParams &p, int64_t q) {
     return c;
 }
 
+// Round 4: templated on the orientation (FWD: KMC_CANON_FORWARD) and on the key
+// width (BIGK: 16 <= k <= 31, so the low dword of the 2k-bit mask is all ones; else
+// k <= 15 and the key fits one dword), and written dword by dword -- the forward key
+// rolled with one funnel shift (v_alignbit) and one shift-or, the reverse
+// complement one funnel shift of the complemented codes per dword -- so that no
+// 64-bit mask, shift or orientation select is left per window (the walks are
+// VALU-bound: K1 24 -> 18 VALU per window).
+template <bool FWD, bool BIGK>
 __device__ __forceinline__ uint32_t chunk_keys(const HParams &p, const ChunkRaw &raw, int64_t q, int64_t ps,
                                                int64_t pe, int64_t rend, unsigned long long (&h)[16]) {
     const int k = p.k;
     const bool soft = p.flags & KMC_CANON_SOFTMASK;
-    const bool fwd_only = p.flags & KMC_CANON_FORWARD;
-    const uint64_t kmask = (1ull << (2 * k)) - 1;
-    const uint64_t wmask = (1ull << k) - 1;
+    // the low 2k bits: mh of the high dword and all of the low one (BIGK), or ml of the low one
+    const uint32_t mh = BIGK ? (uint32_t)((1ull << (2 * k - 32)) - 1ull) : 0u;
+    const uint32_t ml = BIGK ? 0xFFFFFFFFu : (uint32_t)((1ull << (2 * k)) - 1ull);
     uint32_t cd[3], bd[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) chunk_codes(raw.r[i], soft, cd[i], bd[i]);
-    const uint64_t lo64 = (uint64_t)cd[0] | ((uint64_t)cd[1] << 32);
     const uint64_t badm = (uint64_t)bd[0] | ((uint64_t)bd[1] << 16) | ((uint64_t)bd[2] << 32);
     const int64_t last = std::min<int64_t>(pe, rend - k);  // window starts < last
     // window starts [ps, last) of this chunk as a mask (32-bit compares: the
@@ -273,9 +268,6 @@ __device__ __forceinline__ uint32_t chunk_keys(const HParams &p, const ChunkRaw 
     const uint32_t lo_m = lo_j <= 0 ? 0xFFFFu : (lo_j >= 16 ? 0u : (0xFFFFu << lo_j) & 0xFFFFu);
     const uint32_t hi_m = hi_j >= 16 ? 0xFFFFu : (hi_j <= 0 ? 0u : (1u << hi_j) - 1u);
     uint32_t vm = lo_m & hi_m;
-    // the MSB-first key of window 0 by bit reversal, then rolled one base per
-    // window: base j + k - 1 enters at the low end, read from t = the chunk's
-    // codes from base k - 1 on (2 <= 2(k - 1) <= 60)
     // windows holding an invalid base: bit j of the smeared mask = OR of badm's bits
     // j .. j+k-1 (log2 k wave-uniform doubling steps per chunk, instead of a 64-bit
     // shift, mask and compare per window)
@@ -288,17 +280,43 @@ __device__ __forceinline__ uint32_t chunk_keys(const HParams &p, const ChunkRaw 
         }
         vm &= ~(uint32_t)sm;
     }
-    (void)wmask;
-    uint64_t fw = reverse_groups(lo64 & kmask, k);
+    // window 0's MSB-first key by bit reversal; window j's last base (j + k - 1) is
+    // bits 2j of tl = the codes from base k - 1 on (2j <= 30: the low dword)
+    const uint64_t lo64 = (uint64_t)cd[0] | ((uint64_t)cd[1] << 32);
+    const uint64_t fw0 = reverse_groups(lo64 & (((uint64_t)mh << 32) | ml), k);
+    uint32_t fl = (uint32_t)fw0, fh = (uint32_t)(fw0 >> 32);
     const int sk = 2 * (k - 1);
-    const uint64_t t = sk == 0 ? lo64 : (lo64 >> sk) | ((uint64_t)cd[2] << (64 - sk));
+    const uint32_t tl = sk < 32 ? __builtin_amdgcn_alignbit(cd[1], cd[0], sk) : __builtin_amdgcn_alignbit(cd[2], cd[1], sk - 32);
+    const uint32_t n0 = ~cd[0], n1 = ~cd[1], n2 = ~cd[2];  // complemented codes: the reverse complement's key
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        const uint64_t le = (j == 0 ? lo64 : ((lo64 >> (2 * j)) | ((uint64_t)cd[2] << (64 - 2 * j)))) & kmask;
-        if (j > 0) fw = ((fw << 2) | ((t >> (2 * j)) & 3u)) & kmask;
-        h[j] = part_of(fwd_only ? fw : (fw < (le ^ kmask) ? fw : (le ^ kmask)));
+        if (j > 0) {  // roll the forward key one base
+            const uint32_t b = (tl >> (2 * j)) & 3u;
+            if (BIGK) {
+                fh = __builtin_amdgcn_alignbit(fh, fl, 30) & mh;
+                fl = (fl << 2) | b;
+            } else {
+                fl = ((fl << 2) | b) & ml;
+            }
+        }
+        const uint64_t f = ((uint64_t)fh << 32) | fl;
+        uint64_t key = f;
+        if (!FWD) {  // the reverse complement's key = the complemented LE code of the window
+            uint32_t rl = j == 0 ? n0 : __builtin_amdgcn_alignbit(n1, n0, 2 * j);
+            uint32_t rh = 0u;
+            if (BIGK) rh = (j == 0 ? n1 : __builtin_amdgcn_alignbit(n2, n1, 2 * j)) & mh;
+            else rl &= ml;
+            const uint64_t r = ((uint64_t)rh << 32) | rl;
+            key = f < r ? f : r;
+        }
+        h[j] = part_of(key);
     }
     return vm;
+}
+
+// Top nb bits (nb <= 15) of a partition value's high dword (nb = 0: 0) -- one v_bfe_u32
+__device__ __forceinline__ uint32_t top_bits(unsigned long long x, int nb) {
+    return __builtin_amdgcn_ubfe((uint32_t)(x >> 32), (uint32_t)(32 - nb), (uint32_t)nb);
 }
 
 // The workgroup's chunk range and its record pieces: f(r, ps, pe, rend).
@@ -329,9 +347,12 @@ __device__ __forceinline__ void for_each_piece(const HParams &p, int64_t *s_firs
 
 __device__ __forceinline__ int coarse_lg(int lg) { return lg < kCoarseLg ? lg : kCoarseLg; }
 
-// K1: windows per (record, list, workgroup) and per (record, coarse bucket, workgroup)
+// K1: windows per (record, list, workgroup) and per (record, coarse bucket, workgroup).
+// Invalid windows add to a per-lane dummy counter past the lists (no branch per window).
+constexpr uint32_t kK1Dummy = 1u << kMaxLg;
+template <bool FWD, bool BIGK>
 __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
-    __shared__ uint32_t c[1 << kMaxLg];
+    __shared__ uint32_t c[(1 << kMaxLg) + 64];
     __shared__ int64_t s_first;
     const int w = blockIdx.x;
     for_each_piece(p, &s_first, [&](int64_t r, int64_t ps, int64_t pe, int64_t rend) {
@@ -347,12 +368,15 @@ __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
             unsigned long long h[16];
             const ChunkRaw cr = KMC_WALK_PF ? nx : chunk_raw(p, q);
             if (KMC_WALK_PF) nx = chunk_raw(p, q + qs);  // the next chunk, in flight
-            const uint32_t vm = chunk_keys(p, cr, q, ps, pe, rend, h);
+            const uint32_t vm = chunk_keys<FWD, BIGK>(p, cr, q, ps, pe, rend, h);
+            const uint32_t dummy = kK1Dummy + (threadIdx.x & 63u);
 #pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if ((vm >> j) & 1u)
-                    __hip_atomic_fetch_add(&c[lg ? (uint32_t)(h[j] >> (64 - lg)) : 0u], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t sel = (uint32_t)__builtin_amdgcn_sbfe((int)vm, j, 1);  // window j valid: all ones
+                uint32_t idx;  // (v_bfi_b32 as asm: the compiler would turn the select into a compare + v_cndmask)
+                asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(idx) : "v"(sel), "v"(top_bits(h[j], lg)), "v"(dummy));
+                __hip_atomic_fetch_add(&c[idx], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
         __syncthreads();
         const int64_t nwg = p.nwg[r];
@@ -583,6 +607,7 @@ struct Ring8 {
 // need 4 barriers per 16 K windows against the staged sort's 3.)
 // K3a: every window's h at its coarse bucket's position (ent_c), or at its list
 // position (ent) for records whose buckets are single lists
+template <bool FWD, bool BIGK>
 __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
     __shared__ unsigned long long s_stage[kRound];
     __shared__ uint32_t s_cnt[2][kMaxBk + 1];
@@ -600,23 +625,18 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
         for (int b = threadIdx.x; b < 2 * (kMaxBk + 1); b += kWalkBlock) (&s_cnt[0][0])[b] = 0u;
         __syncthreads();
         uint64_t *dst = lg > lgc ? p.ent_c : p.ent;
-        const auto bk = [lgc](unsigned long long x) { return lgc ? (uint32_t)(x >> (64 - lgc)) : 0u; };
+        const auto bk = [lgc](unsigned long long x) { return top_bits(x, lgc); };
         const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
         ChunkRaw nx;
         if (KMC_WALK_PF) nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
-        // (K3A_PREWAIT: the first chunk waited for here too, so that nothing is left
-        // pending on either path into the loop and its top needs no wait -- which
-        // would also wait for the previous round's stores)
-        if (KMC_K3A_PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);
         for (int64_t cb = c0; cb < c1; cb += kWalkBlock) {
             const int64_t c = cb + threadIdx.x;
             unsigned long long h[16];
             uint32_t vm = 0u;
             ChunkRaw cr = nx;
-            if (!KMC_WALK_PF && c < c1) cr = chunk_raw(p, c << 4);
+            if (!KMC_WALK_PF) cr = chunk_raw(p, c << 4);
             if (KMC_WALK_PF) nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
-            if (c < c1) vm = chunk_keys(p, cr, c << 4, ps, pe, rend, h);
-            if (KMC_K3A_PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
+            vm = chunk_keys<FWD, BIGK>(p, cr, c << 4, ps, pe, rend, h);  // (past the piece: vm = 0, h defined)
             if (lg > lgc)
                 staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return x; }, dst);
             else  // buckets are the lists
@@ -682,11 +702,10 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
         for (int j = 0; j < 8; ++j) {
             const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
             vm |= i < a1 ? 1u << j : 0u;
-            bk[j] = (uint32_t)(x[j] >> (64 - lg)) & (uint32_t)(F - 1);
+            bk[j] = __builtin_amdgcn_ubfe((uint32_t)(x[j] >> 32), (uint32_t)(32 - lg), (uint32_t)lf);  // list bits below the bucket's
             v[j] = list_value(x[j]);
         }
         rg.add<8>(v, bk, vm);
-        if (KMC_K3B_PREWAIT) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
         rg.round_end();
     }
     rg.finish();
@@ -1037,6 +1056,15 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
     reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
     lds_barrier();  // A: counters zero; the previous list is done
+    // Round 4: every key of the list waited for here, outside any branch.  The
+    // loads above and the uses below sit in per-key branches, so the compiler's
+    // wait tracking lost them at the joins and waited vmcnt(0) before every key's
+    // use -- in the scatter, right after the previous key's emit store: a store
+    // acknowledgement per key (gfx9 counts stores in vmcnt).  Same box: K4s
+    // 15.45-15.55 -> 15.05-15.16 ms on C4 (profiles/r04g_c4_ab.txt).  Issuing the
+    // rank adds and the scatter's slot reads all before their first use, and one
+    // output reservation per wave, measured no further change and was not kept.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
     if (tid == 0) {
         S.out = 0u;
         S.nhot = 0u;
@@ -1268,6 +1296,26 @@ uint32_t h_sort_cap = kSortCap;
 uint32_t h_sort_cap_big = kSortCapBig;
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// K1 / K3a instances by orientation and key width
+struct WalkCount {
+    template <bool F, bool B>
+    static void go(const HParams &p, hipStream_t st) {
+        hipLaunchKernelGGL((canon_count_kernel<F, B>), dim3(p.G), dim3(kWalkBlock), 0, st, p);
+    }
+};
+struct WalkCoarse {
+    template <bool F, bool B>
+    static void go(const HParams &p, hipStream_t st) {
+        hipLaunchKernelGGL((canon_coarse_kernel<F, B>), dim3(p.G), dim3(kWalkBlock), 0, st, p);
+    }
+};
+template <class W>
+void launch_walk(const HParams &p, hipStream_t st) {
+    const bool fwd = p.flags & KMC_CANON_FORWARD, big = p.k >= 16;
+    if (fwd) big ? W::template go<true, true>(p, st) : W::template go<true, false>(p, st);
+    else big ? W::template go<false, true>(p, st) : W::template go<false, false>(p, st);
+}
 
 }  // namespace
 }  // namespace kmc
@@ -1532,11 +1580,11 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
         if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream)) ||
             (he = hipMemsetAsync(p.cnt_c, 0, (size_t)Mc * 4, stream)))
             return (int)he;
-        hipLaunchKernelGGL(canon_count_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
+        launch_walk<WalkCount>(p, stream);
     }
     excl_scan_u32(p.cnt, M, bsum, p.off, stream);
     excl_scan_u32(p.cnt_c, Mc, bsum, p.off_c, stream);
-    hipLaunchKernelGGL(canon_coarse_kernel, dim3(p.G), dim3(kWalkBlock), 0, stream, p);
+    launch_walk<WalkCoarse>(p, stream);
     hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (NF > 0) hipLaunchKernelGGL(canon_fine_kernel, dim3((unsigned)NF), dim3(kWalkBlock), 0, stream, p);
     // persistent, two workgroups per CU (64 KB of LDS each), striding over the lists

@@ -1,7 +1,10 @@
 # GPU (round 4): same-box A/B of this round's walk and launch changes, then parity.
 #  1. C4 (cbench, parity-checked): lib/variants/libkmc_k3base.so (canonical walks
 #     before the change) against the new build (templated K1 / K3a, branch-free
-#     K1 adds and K3a staged round, batched K3a write-out), two alternating rounds;
+#     K1 adds and K3a staged round, batched K3a write-out; k4w0: that, with K4s as
+#     before; k4b0: + K4s's explicit key wait; plb0: all but the place kernel's
+#     batched count loads; new: everything),
+#     two alternating rounds;
 #  2. one rank's step of an N-way job (shardbench, N = 1 and 8): dvec0 (dense
 #     launch as before) against dvec1 (parallel first-record search, 16-byte LDS
 #     clear and slab flush), two alternating rounds;
@@ -13,7 +16,7 @@ M=$PWD/dna-kmeres-parallel_amd/lib/libkmc.so
 PT="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
 if [ -z "$SKIPC4" ]; then
 for r in 1 2; do
-  for v in k3base new; do
+  for v in ${C4V:-k3base k4w0 k4b0 plb0 new}; do
     L=$V/libkmc_$v.so; [ $v = new ] && L=$M
     KMC_LIB=$L run 400 rocprofv3 --kernel-trace --output-format csv -d $O/$v$r -o t -- python3 scripts/cbench.py --configs c4 --iters 3 --cpu-sample-c4 0 > $O/$v$r.log 2>&1
     echo "== $v $r $(grep -o '"s_med": [0-9.]*' $O/$v$r.log | tr '\n' ' ')"; python3 scripts/trace_kernels.py $O/$v$r canon_
