@@ -58,7 +58,9 @@ def random_records(rng, lens, alphabet=b"ACGTN", p=(.2475, .2475, .2475, .2475, 
 def test_canonical_golden(kmc, oracle, cuda, name, dialect):
     g = G.load(name, dialect)
     idx = G.full_indices(g)
-    for k in (1, 3, 5, 12, 21, 31):
+    # (15 / 16: the two key-width instances of the walks, either side of the
+    # dword boundary of the 2k-bit key)
+    for k in (1, 3, 5, 12, 15, 16, 21, 31):
         for flags in (0, kmc.CANON_SOFTMASK, kmc.CANON_FORWARD):
             got = gpu_canon(kmc, cuda, g["data"], idx, k, flags)
             exp = oracle.count_canonical(g["data"], idx, k, soft=bool(flags & 1), forward=bool(flags & 2))
@@ -87,7 +89,7 @@ def test_forward_mode_equals_dense_path(kmc, cuda, k):
     np.testing.assert_array_equal(rebuilt, dense)
 
 
-@pytest.mark.parametrize("k", [11, 25, 31])
+@pytest.mark.parametrize("k", [11, 15, 16, 25, 31])
 def test_canonical_random_vs_oracle(kmc, oracle, cuda, k):
     """Ragged records (empty, shorter than k, tiny, long), N runs, lowercase."""
     rng = np.random.default_rng(100 + k)
