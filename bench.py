@@ -66,7 +66,7 @@ def parse(argv=None):
                     help="N > 1: all-reduces timed alone after the timed region")
     ap.add_argument("--reserve-cus", type=int, default=-1,
                     help="CUs left out of the histogram grid for the overlapped all-reduce, whose RCCL "
-                         "channels are capped to match (NCCL_MAX_NCHANNELS); -1 = 8 at N > 1, 0 at N = 1")
+                         "channels are capped to match (NCCL_MAX_NCHANNELS); -1 = 4 at N > 1, 0 at N = 1")
     return ap.parse_args(argv)
 
 
@@ -287,7 +287,11 @@ def main():
     # step at 8-way with 8 CUs held for 50 us, scripts/interfere.py).  Leaving
     # reserve_cus CUs to RCCL, its channels capped to as many, keeps them apart
     # (the same experiment: 0.348-0.351 -> 0.318 ms; 0.311 -> 0.318 ms alone).
-    reserve = args.reserve_cus if args.reserve_cus >= 0 else (8 if world > 1 else 0)
+    # Round 4 (profiles/r04k_interfere_reserve.log): 4 CUs cost less alone (0.305
+    # against 0.311 ms) and held the step at 0.309-0.310 ms in 3 of 4 stand-in runs,
+    # where 8 did not (0.349-0.352 ms); 4 RCCL channels carry the 2.6 MB (C2) or
+    # 21 MB (C5) all-reduce well inside one step.
+    reserve = args.reserve_cus if args.reserve_cus >= 0 else (4 if world > 1 else 0)
     if world > 1 and reserve > 0:
         os.environ.setdefault("NCCL_MAX_NCHANNELS", str(reserve))
     kmc.set_reserved_cus(reserve)
