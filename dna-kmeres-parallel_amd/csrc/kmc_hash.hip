@@ -985,6 +985,9 @@ using SortBig = SortCfg<1024, 12, 12288, 14>;   // LDS: 1 workgroup per CU
 constexpr int kSortBlock = SortSmall::kBlock;
 constexpr uint32_t kSortCap = SortSmall::kCap;
 constexpr uint32_t kSortCapBig = SortBig::kCap;
+#ifndef KMC_K4S_PF
+#define KMC_K4S_PF 1
+#endif
 #ifndef KMC_SORT_MAXM
 #define KMC_SORT_MAXM 8
 #endif
@@ -998,6 +1001,7 @@ struct K4sLds {
     uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
     uint16_t q[C::kBlock / 64][C::kRes * 64];  // per wave: positions of keys that share a slot
     uint32_t wsum[C::kBlock / 64];
+    uint32_t pfs[64];                 // scratch target of the next list's L2 prefetch (never read)
     uint32_t out;                     // distinct keys emitted
     uint32_t nhot;
 };
@@ -1041,7 +1045,7 @@ __device__ __forceinline__ uint32_t slot_start(const K4sLds<C> &S, uint32_t sl, 
 // to the table kernel.
 template <class C>
 __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_t l, uint64_t b0, uint64_t e0,
-                                          uint32_t n) {
+                                          uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0) {
     constexpr int kRes = C::kRes, kBlk = C::kBlock, kSlots = C::kSlots;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1052,6 +1056,15 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     for (int j = 0; j < kRes; ++j) {
         const uint32_t i = (uint32_t)(j * kBlk + tid);
         kh[j] = i < n ? p.ent[b0 + i] : kEmptyH;
+    }
+    // the bounds of the workgroup's next list (nxt: its begin and end, or null),
+    // loaded with the keys so that they cost no wait of their own; the caller
+    // starts the next list with them instead of loading them there (a dependent
+    // round trip before that list's key loads)
+    nb0 = ne0 = 0;
+    if (nxt) {
+        nb0 = nxt[0];
+        ne0 = nxt[1];
     }
     reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(0u, 0u, 0u, 0u);
     reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(0u, 0u, 0u, 0u);
@@ -1065,6 +1078,23 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     // rank adds and the scatter's slot reads all before their first use, and one
     // output reservation per wave, measured no further change and was not kept.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
+    if (KMC_K4S_PF && nxt) {
+        // (round 4) the workgroup's next list [nb0, ne0) touched once per 128-byte
+        // line now, so that its key loads above find it in L2 / MALL one list later
+        // (same box: K4s 15.1 -> 14.5 ms on C4).  An LDS-DMA dword per line into a
+        // scratch block nothing reads, written as asm: no register receives it, and
+        // the compiler, which does not see it, neither sinks it to a use nor makes
+        // later LDS accesses wait for it (the builtin did both).  An operation it
+        // does not count only makes its own vmcnt waits stricter (completion is in
+        // order), and the next list's vmcnt(0) above retires it; the last list
+        // prefetches nothing, so none is in flight when the workgroup ends.
+        const uint64_t nn = ne0 - nb0 <= (uint64_t)C::kCap ? ne0 - nb0 : 0;  // (longer: another kernel's)
+        if ((uint64_t)tid * 16u < nn) {
+            const uint64_t a = (uint64_t)(p.ent + nb0 + (uint64_t)tid * 16u);
+            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(a), "s"(lds_off(&S.pfs[0]))
+                         : "m0", "memory");
+        }
+    }
     if (tid == 0) {
         S.out = 0u;
         S.nhot = 0u;
@@ -1222,17 +1252,31 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
 __global__ __launch_bounds__(SortSmall::kBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_sort_kernel(
     HParams p) {
     __shared__ __attribute__((aligned(16))) K4sLds<SortSmall> S;
+    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)
+    if ((int64_t)blockIdx.x < p.lists) {
+        b0 = p.list_start[blockIdx.x];
+        e0 = p.list_start[blockIdx.x + 1];
+    }
     for (int64_t l = blockIdx.x; l < p.lists; l += gridDim.x) {
-        const uint64_t b0 = p.list_start[l], e0 = p.list_start[l + 1];
         const uint32_t n = (uint32_t)(e0 - b0 < 0xFFFFFFFFull ? e0 - b0 : 0xFFFFFFFFull);
+        const uint64_t *nxt = l + gridDim.x < p.lists ? p.list_start + l + gridDim.x : nullptr;
         if (n > p.sort_cap) {  // workgroup-uniform
             if (threadIdx.x == 0) {
                 if (n <= p.sort_cap_big) queue_list(p.big, p.nbig, l, b0, e0);
                 else defer_list(p, l, b0, e0);
             }
+            if (nxt) {
+                b0 = nxt[0];
+                e0 = nxt[1];
+            }
             continue;
         }
-        sort_list<SortSmall>(p, S, l, b0, e0, n);
+        // (the next list of this workgroup: its bounds loaded and its keys
+        // prefetched into L2 during this one)
+        uint64_t nb0, ne0;
+        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0);
+        b0 = nb0;
+        e0 = ne0;
     }
 }
 
@@ -1243,7 +1287,10 @@ __global__ __launch_bounds__(SortBig::kBlock) void canon_sort_big_kernel(HParams
     const int64_t nl = (int64_t)*p.nbig;
     for (int64_t i = blockIdx.x; i < nl; i += gridDim.x) {
         const uint64_t b0 = p.big[3 * i + 1], e0 = p.big[3 * i + 2];
-        sort_list<SortBig>(p, S, (int64_t)p.big[3 * i], b0, e0, (uint32_t)(e0 - b0));
+        const int64_t in = i + gridDim.x;
+        uint64_t nb0, ne0;  // (few lists here: the entries are reloaded per list)
+        sort_list<SortBig>(p, S, (int64_t)p.big[3 * i], b0, e0, (uint32_t)(e0 - b0), in < nl ? p.big + 3 * in + 1 : nullptr,
+                           nb0, ne0);
     }
 }
 
