@@ -549,7 +549,12 @@ struct Ring8 {
             }
         }
     }
-    // Phase B (the caller brackets it with barriers).
+    // Phase B (the caller brackets it with barriers).  Round 4: complete segments
+    // leave as whole 64-byte stores by lane quads, as R3's do -- in pass t every
+    // quad stores the segment of its lane t, 16 bytes per lane, its ring chunk and
+    // list position broadcast by DPP -- instead of each lane storing its own
+    // segment in four 16-byte pieces (64 scattered pieces per store instruction,
+    // about half the HBM write rate: scripts/write_microbench.hip).
     __device__ __forceinline__ void flush() {
         const uint32_t b = bucket_of_thread(), j = member(), tpb = 1u << (10 - lgb);
         const uint32_t f0 = (uint32_t)F & 7u;
@@ -559,25 +564,31 @@ struct Ring8 {
         const unsigned long long top = F1 < H + R ? F1 : H + R;
         const uint32_t nseg = (uint32_t)((top - H) >> 3);
         const uint32_t rt = rot(b);
-        const uint4 *row = reinterpret_cast<const uint4 *>(&L->ring[b << rlg]);  // 2 entries per uint4
-        const uint32_t cm = (R >> 1) - 1u;  // chunk index mask
-        for (uint32_t i = j; i < nseg; i += tpb) {
+        const uint32_t q = threadIdx.x & 3u;
+        const uint4 *ring4 = reinterpret_cast<const uint4 *>(&L->ring[0]);  // 2 entries per uint4
+        for (uint32_t i = j; __any(i < nseg); i += tpb) {  // (wave-uniform trip count: the quads need every lane)
             const unsigned long long g0 = H + 8ull * i;
-            if (g0 >= V) {
-                const uint32_t c0 = (((uint32_t)g0 + rt) & rmask()) >> 1;
-                const uint32_t sh = ((b >> 2) + (i >> 2)) & 3u;  // rotated chunk order: spread the banks
-                const uint32_t q0 = sh, q1 = (sh + 1) & 3u, q2 = (sh + 2) & 3u, q3 = (sh + 3) & 3u;
-                const uint4 v0 = row[(c0 + q0) & cm], v1 = row[(c0 + q1) & cm];
-                const uint4 v2 = row[(c0 + q2) & cm], v3 = row[(c0 + q3) & cm];
-                uint4 *o = reinterpret_cast<uint4 *>(dst + g0);
-                o[q0] = v0;
-                o[q1] = v1;
-                o[q2] = v2;
-                o[q3] = v3;
-            } else {
-                for (uint32_t q = 0; q < 8; ++q)
-                    if (g0 + q >= V) dst[g0 + q] = L->ring[(b << rlg) + (((uint32_t)(g0 + q) + rt) & rmask())];
+            const bool seg = i < nseg;
+            if (seg && g0 < V) {  // partly before V (a piece start after an overflow): entry by entry
+                for (uint32_t e = 0; e < 8; ++e)
+                    if (g0 + e >= V) dst[g0 + e] = L->ring[(b << rlg) + (((uint32_t)(g0 + e) + rt) & rmask())];
             }
+            // this lane's segment: uint4 index of its chunk 0 in the ring (bit 31: a
+            // whole segment to store) and its list position / 8
+            const uint32_t c0 = ((b << rlg) + (((uint32_t)g0 + rt) & rmask())) >> 1;
+            const uint32_t A = c0 | (seg && g0 >= V ? 0x80000000u : 0u);
+            const uint64_t gs = g0 >> 3;
+            uint32_t a[4], glo[4], ghi[4];
+            quad_bcast4(A, a);
+            quad_bcast4((uint32_t)gs, glo);
+            quad_bcast4((uint32_t)(gs >> 32), ghi);
+            uint4 v[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = ring4[(a[t] & 0x7FFFFFFFu) + q];  // (a quad without a segment reads harmlessly)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (a[t] & 0x80000000u)
+                    reinterpret_cast<uint4 *>(dst + 8ull * ((uint64_t)glo[t] | ((uint64_t)ghi[t] << 32)))[q] = v[t];
         }
         if (F1 > H + R) V = F1;  // [H + R, F1) went straight to dst
         F = F1;

@@ -322,14 +322,6 @@ struct RingGeom {
     static_assert(2 * (BLOCK * 16 * KMC_RING_RT + 32) < 65536, "one tile per wave per round");
 };
 
-// o[t] = x of lane t of this lane's quad (DPP quad_perm broadcasts)
-__device__ __forceinline__ void quad_bcast4(uint32_t x, uint32_t *o) {
-    o[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x00, 0xF, 0xF, false);
-    o[1] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x55, 0xF, 0xF, false);
-    o[2] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xAA, 0xF, 0xF, false);
-    o[3] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xFF, 0xF, 0xF, false);
-}
-
 // slot swizzle of bucket b (XOR mask, a multiple of 8 slots below 64)
 __device__ __forceinline__ uint32_t ring_swz(uint32_t b) { return ((b >> 1) & 7u) * 8u; }
 

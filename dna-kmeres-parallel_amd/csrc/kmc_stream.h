@@ -133,6 +133,14 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 
 // Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for
 // the wave's outstanding global loads, so the tile prefetch keeps streaming.
+// o[t] = x of lane t of this lane's quad (DPP quad_perm broadcasts: VALU, no LDS)
+__device__ __forceinline__ void quad_bcast4(uint32_t x, uint32_t *o) {
+    o[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x00, 0xF, 0xF, false);
+    o[1] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x55, 0xF, 0xF, false);
+    o[2] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xAA, 0xF, 0xF, false);
+    o[3] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xFF, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
