@@ -643,6 +643,28 @@ def test_bench_rank_counts_sum_to_whole(kmc, oracle, cuda, scaling, world, recor
     np.testing.assert_array_equal(acc, exp)
 
 
+@pytest.mark.parametrize("k,n", [(4, 511), (4, 512), (4, 513), (8, 1023), (8, 1024), (8, 1025)])
+def test_first_record_search_at_block_size(kmc, oracle, cuda, k, n):
+    """A workgroup finds the record its range starts in by one index load per
+    thread when the records fit one block (n <= threads: 512 at k = 4, 1024 at
+    k = 8), else by a binary search: record counts either side of that boundary,
+    lengths such that workgroup ranges start in records all over the buffer, every
+    record against the oracle."""
+    import torch
+    rng = np.random.default_rng(700 + n)
+    lens = rng.integers(0, 9000, size=n)
+    lens[::7] = 0
+    data, idx = random_records(rng, lens, 0.002, 0.002, 0.0005)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    out = torch.full((1 << (2 * k), n), -1, dtype=torch.int32, device=cuda)
+    inv = torch.full((n,), -1, dtype=torch.int32, device=cuda)
+    kmc.count_dense_ex(kmc.dense_args(d, di, k, out, invalid=inv))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv)
+
+
 @pytest.mark.parametrize("k,n", [(8, 70_000), (9, 65_600)])
 def test_many_short_records(kmc, oracle, cuda, k, n):
     """More records than one grid dimension of the per-record helper kernels can
