@@ -962,10 +962,12 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
 
 // K4s (round 2): the common list, n <= sort_cap keys with no key repeated more than
 // kSortMaxM times, counted by a counting sort in LDS instead of the probed table:
-//   rank     one returning LDS add per key on its slot's 16-bit counter (slot =
-//            the low kSortSlotsLg bits of h, uniform: the list is cut by other bits)
-//   scan     exclusive prefix of the 8 192 counters (16 per thread, one block scan)
-//   scatter  key -> sk[start(slot) + rank]: the list sorted by slot
+//   rank     one returning LDS add per key on its slot's word (slot = the low
+//            kSlotsLg bits of h, uniform: the list is cut by other bits), which
+//            counts the slot's keys and tests them for distinctness (round 4)
+//   scan     exclusive prefix of the 4 096 counts (8 per thread, one block scan)
+//   scatter  a key of a distinct slot leaves with count 1; the others go to
+//            sk[start(slot) + rank]: those keys sorted by slot
 //   dedup    position p (p = tid + 512 j: a wave reads consecutive keys) compares
 //            its key with the other keys of its slot (m - 1 of them, m ~ Poisson(<1));
 //            the first occurrence is emitted with the slot's count of its key,
@@ -978,7 +980,7 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
 // canon_table_kernel, which handles any length and any repeat count.
 // Two instances (round 4): the common one, two 512-thread workgroups per CU, takes
 // lists of up to 6 080 keys; a big one, one 1 024-thread workgroup per CU with a
-// 16 384-slot counter table, takes the lists of 6 081 .. 12 288 keys that the
+// 8 192-slot table, takes the lists of 6 081 .. 12 288 keys that the
 // first hands it (chromosome-sized records: 2^15 lists of ~7.6 K keys), which
 // until round 3 went to the probed table kernel.
 template <int BLOCK, int RES, uint32_t CAP, int SLOTS_LG>
@@ -987,12 +989,12 @@ struct SortCfg {
     static constexpr int kRes = RES;                    // keys per thread
     static constexpr uint32_t kCap = CAP;               // <= kBlock * kRes
     static constexpr int kSlotsLg = SLOTS_LG;
-    static constexpr int kSlots = 1 << SLOTS_LG;        // 16-bit counters, two per word
-    static_assert(CAP <= (uint32_t)(BLOCK * RES) && CAP < 65536u, "K4s sizes");
-    static_assert(kSlots / 2 == BLOCK * 8, "K4s scan: 8 counter words per thread");
+    static constexpr int kSlots = 1 << SLOTS_LG;        // one 32-bit word per slot
+    static_assert(CAP <= (uint32_t)(BLOCK * RES) && CAP < 32768u, "K4s sizes");
+    static_assert(kSlots == BLOCK * 8, "K4s scan: 8 slot words per thread");
 };
-using SortSmall = SortCfg<512, 12, 6080, 13>;   // LDS: 2 workgroups per CU
-using SortBig = SortCfg<1024, 12, 12288, 14>;   // LDS: 1 workgroup per CU
+using SortSmall = SortCfg<512, 12, 6080, 12>;   // LDS: 2 workgroups per CU
+using SortBig = SortCfg<1024, 12, 12288, 13>;   // LDS: 1 workgroup per CU
 constexpr int kSortBlock = SortSmall::kBlock;
 constexpr uint32_t kSortCap = SortSmall::kCap;
 constexpr uint32_t kSortCapBig = SortBig::kCap;
@@ -1008,7 +1010,7 @@ constexpr uint32_t kHotMax = 128;                     // crowded slots per list 
 template <class C>
 struct K4sLds {
     unsigned long long sk[C::kCap];   // the list, sorted by slot
-    uint32_t sc[C::kSlots / 2];       // slot counters, then slot starts (16-bit, packed)
+    uint32_t sc[C::kSlots];           // slot words: count | sub-hash sum, then start | count | distinct
     uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
     uint16_t q[C::kBlock / 64][C::kRes * 64];  // per wave: positions of keys that share a slot
     uint32_t wsum[C::kBlock / 64];
@@ -1044,12 +1046,10 @@ __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned
 
 __device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t hi) { return hi ? (w >> 16) : (w & 0xFFFFu); }
 
-
-// start of slot sl's keys in sk (after the scan); slot kSlots ends at n
-template <class C>
-__device__ __forceinline__ uint32_t slot_start(const K4sLds<C> &S, uint32_t sl, uint32_t n) {
-    return sl < (uint32_t)C::kSlots ? half16(S.sc[sl >> 1], sl & 1u) : n;
-}
+// A slot word after the scan: the slot's start in sk (bits 0-15), its key count
+// (16-30) and bit 31 set when its keys are known to be distinct (section 4.4).
+constexpr uint32_t kSlotDistinct = 0x80000000u;
+__device__ __forceinline__ uint32_t slot_count(uint32_t w) { return (w >> 16) & 0x7FFFu; }
 
 // One list of n <= C::kCap keys [b0, e0) counted by the counting sort (the
 // workgroup calls it uniformly).  A list with too many crowded slots is deferred
@@ -1110,37 +1110,44 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         S.out = 0u;
         S.nhot = 0u;
     }
-    // rank: one returning add per key on its slot's 16-bit counter
+    // rank: one returning add per key on its slot's word, 1 + 2^(16 + sub) with sub
+    // four more bits of the key's hash: the low half counts the slot's keys (the
+    // key's rank), the high half sums one power of two per key.  A sum of m powers
+    // of two has m bits set only if no two are equal (every carry, and every bit
+    // carried out of the word, leaves fewer), so popcount(high) == count proves the
+    // slot's keys distinct: each is a key of count 1, as a key alone in its slot.
+    // Only the slots that fail the test (a repeated key, or two keys on the same
+    // sub: ~6 % of the keys at 0.75 keys per slot, against 31 % of the keys sharing
+    // a slot with twice the slots) are sorted and compared key by key.
     uint32_t rk[kRes / 2];  // ranks (< 2^16), two per register
 #pragma unroll
     for (int j = 0; j < kRes; ++j) {
         if ((j & 1) == 0) rk[j >> 1] = 0u;
         if ((uint32_t)(j * kBlk + tid) < n) {
-            const uint32_t sl = (uint32_t)kh[j] & (kSlots - 1);
-            const uint32_t o = __hip_atomic_fetch_add(&S.sc[sl >> 1], (sl & 1u) ? 0x10000u : 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-            rk[j >> 1] |= half16(o, sl & 1u) << (16 * (j & 1));
+            const uint32_t lo = (uint32_t)kh[j];
+            const uint32_t sl = lo & (kSlots - 1);
+            const uint32_t inc = 1u + (0x10000u << __builtin_amdgcn_ubfe(lo, C::kSlotsLg, 4));
+            const uint32_t o = __hip_atomic_fetch_add(&S.sc[sl], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            rk[j >> 1] |= (o & 0xFFFFu) << (16 * (j & 1));
         }
     }
     lds_barrier();  // B: every key ranked
-    // scan: thread t owns counter words 8t .. 8t+7 (slots 16t .. 16t+15)
+    // scan: thread t owns slot words 8t .. 8t+7; a slot of distinct keys takes
+    // no room in sk
     const uint4 w0 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid];
     const uint4 w1 = reinterpret_cast<const uint4 *>(S.sc)[2 * tid + 1];
     uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
     uint32_t run = 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint32_t c0 = w[i] & 0xFFFFu, c1 = w[i] >> 16;
-        if (__builtin_expect(c0 > kSortMaxM, 0)) {
+        const uint32_t c = w[i] & 0xFFFFu;
+        const bool dist = (uint32_t)__builtin_popcount(w[i] >> 16) == c;
+        if (__builtin_expect(!dist && c > kSortMaxM, 0)) {
             const uint32_t x = atomicAdd(&S.nhot, 1u);
-            if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i;
+            if (x < kHotMax) S.hot[x] = 8u * tid + i;
         }
-        if (__builtin_expect(c1 > kSortMaxM, 0)) {
-            const uint32_t x = atomicAdd(&S.nhot, 1u);
-            if (x < kHotMax) S.hot[x] = 16u * tid + 2u * i + 1u;
-        }
-        w[i] = run | ((run + c0) << 16);  // exclusive starts, relative to the thread
-        run += c0 + c1;
+        w[i] = run | (c << 16) | (dist ? kSlotDistinct : 0u);  // exclusive start, relative to the thread
+        run += dist ? 0u : c;
     }
     uint32_t incl = run;
 #pragma unroll
@@ -1153,9 +1160,8 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     uint32_t base = incl - run;
 #pragma unroll
     for (int v = 0; v < kBlk / 64; ++v) base += v < wv ? S.wsum[v] : 0u;
-    const uint32_t bb = base | (base << 16);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] += bb;  // starts < 2^16: no carry between the halves
+    for (int i = 0; i < 8; ++i) w[i] += base;  // starts < 2^15: no carry into the count
     reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
     reinterpret_cast<uint4 *>(S.sc)[2 * tid + 1] = make_uint4(w[4], w[5], w[6], w[7]);
     lds_barrier();  // C2: slot starts
@@ -1164,21 +1170,21 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         if (tid == 0) defer_list(p, l, b0, e0);
         return;  // (the next list's barrier A orders the LDS reuse)
     }
-    // scatter: a key alone in its slot (the common case: ~4 K keys over 8 192
-    // slots) is a distinct key of count 1 and leaves at once; the others go to
-    // sk, and those of slots with at most kSortMaxM keys to this wave's queue
-    // of keys to check against their slot
+    // scatter: a key of a distinct slot (alone in it, or all its keys on
+    // different subs: ~94 % of the keys of distinct 2-4 K-key lists over 4 096
+    // slots) is a key of count 1 and leaves at once; the others go to sk, and
+    // those of slots with at most kSortMaxM keys to this wave's queue of keys to
+    // check against their slot
     uint32_t qn = 0u;  // wave-uniform
 #pragma unroll
     for (int j = 0; j < kRes; ++j) {
         bool alone = false, shared = false;
         uint32_t pos = 0u;
         if ((uint32_t)(j * kBlk + tid) < n) {
-            const uint32_t sl = (uint32_t)kh[j] & (kSlots - 1);
-            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u);
-            const uint32_t m = slot_start(S, sl + 1u, n) - a;
-            pos = a + half16(rk[j >> 1], j & 1);
-            alone = m == 1u;
+            const uint32_t sw = S.sc[(uint32_t)kh[j] & (kSlots - 1)];
+            const uint32_t m = slot_count(sw);
+            pos = (sw & 0xFFFFu) + half16(rk[j >> 1], j & 1);
+            alone = (sw & kSlotDistinct) != 0u;
             if (!alone) {
                 S.sk[pos] = kh[j];
                 shared = m <= kSortMaxM;
@@ -1206,8 +1212,8 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         if (act) {
             const uint32_t pos = wq[q0 + lane];
             h = S.sk[pos];
-            const uint32_t sl = (uint32_t)h & (kSlots - 1);
-            const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
+            const uint32_t sw = S.sc[(uint32_t)h & (kSlots - 1)];
+            const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);
             first = true;
             for (uint32_t q = a; q < e; ++q) {  // 2 <= m <= kSortMaxM
                 if (q != pos && S.sk[q] == h) {
@@ -1226,8 +1232,8 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     // per wave: each round takes the first key not yet counted as the pivot, counts
     // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
     for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kBlk / 64) {
-        const uint32_t sl = S.hot[hs];
-        const uint32_t a = half16(S.sc[sl >> 1], sl & 1u), e = slot_start(S, sl + 1u, n);
+        const uint32_t sw = S.sc[S.hot[hs]];
+        const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);
         uint32_t c = a;
         for (;;) {
             unsigned long long piv = kEmptyH;
