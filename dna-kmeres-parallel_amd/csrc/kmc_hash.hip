@@ -1012,7 +1012,6 @@ struct K4sLds {
     unsigned long long sk[C::kCap];   // the list, sorted by slot
     uint32_t sc[C::kSlots];           // slot words: count | sub-hash sum, then start | count | distinct
     uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
-    uint16_t q[C::kBlock / 64][C::kRes * 64];  // per wave: positions of keys that share a slot
     uint32_t wsum[C::kBlock / 64];
     uint32_t pfs[64];                 // scratch target of the next list's L2 prefetch (never read)
     uint32_t out;                     // distinct keys emitted
@@ -1061,7 +1060,6 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint16_t *wq = S.q[wv];
     unsigned long long kh[kRes];
 #pragma unroll
     for (int j = 0; j < kRes; ++j) {
@@ -1157,9 +1155,13 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     }
     if (lane == 63) S.wsum[wv] = incl;
     lds_barrier();  // C1: wave totals
-    uint32_t base = incl - run;
+    uint32_t base = incl - run, nsk = 0u;  // nsk: keys of the slots that failed the test
 #pragma unroll
-    for (int v = 0; v < kBlk / 64; ++v) base += v < wv ? S.wsum[v] : 0u;
+    for (int v = 0; v < kBlk / 64; ++v) {
+        const uint32_t x = S.wsum[v];
+        base += v < wv ? x : 0u;
+        nsk += x;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] += base;  // starts < 2^15: no carry into the count
     reinterpret_cast<uint4 *>(S.sc)[2 * tid] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -1172,23 +1174,14 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     }
     // scatter: a key of a distinct slot (alone in it, or all its keys on
     // different subs: ~94 % of the keys of distinct 2-4 K-key lists over 4 096
-    // slots) is a key of count 1 and leaves at once; the others go to sk, and
-    // those of slots with at most kSortMaxM keys to this wave's queue of keys to
-    // check against their slot
-    uint32_t qn = 0u;  // wave-uniform
+    // slots) is a key of count 1 and leaves at once; the others go to sk
 #pragma unroll
     for (int j = 0; j < kRes; ++j) {
-        bool alone = false, shared = false;
-        uint32_t pos = 0u;
+        bool alone = false;
         if ((uint32_t)(j * kBlk + tid) < n) {
             const uint32_t sw = S.sc[(uint32_t)kh[j] & (kSlots - 1)];
-            const uint32_t m = slot_count(sw);
-            pos = (sw & 0xFFFFu) + half16(rk[j >> 1], j & 1);
             alone = (sw & kSlotDistinct) != 0u;
-            if (!alone) {
-                S.sk[pos] = kh[j];
-                shared = m <= kSortMaxM;
-            }
+            if (!alone) S.sk[(sw & 0xFFFFu) + half16(rk[j >> 1], j & 1)] = kh[j];
         }
         const uint64_t am = __ballot(alone);
         if (am) {
@@ -1197,25 +1190,22 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
             wb = (uint32_t)__shfl((int)wb, 0);
             if (alone) emit_pair(p, b0 + wb + (uint32_t)__popcll(am & lt), kh[j], 1u);
         }
-        const uint64_t sm = __ballot(shared);
-        if (shared) wq[qn + (uint32_t)__popcll(sm & lt)] = (uint16_t)pos;
-        qn += (uint32_t)__popcll(sm);
     }
-    lds_barrier();  // D: the shared keys sorted by slot
-    // the wave's queued keys, 64 at a time: the first occurrence in its slot is
-    // emitted with the slot's count of its key
-    for (uint32_t q0 = 0; q0 < qn; q0 += 64) {
-        const bool act = q0 + (uint32_t)lane < qn;
+    lds_barrier();  // D: the keys of the failing slots sorted by slot
+    // those keys, sk[0, nsk), spread over all threads: a key of a slot of at most
+    // kSortMaxM keys is compared with the others of its slot, and the first
+    // occurrence is emitted with the slot's count of its key (crowded slots: below)
+    for (uint32_t p0 = 0; p0 < nsk; p0 += kBlk) {  // workgroup-uniform
+        const uint32_t pos = p0 + (uint32_t)tid;
         bool first = false;
         uint32_t cnt = 1u;
         unsigned long long h = 0;
-        if (act) {
-            const uint32_t pos = wq[q0 + lane];
+        if (pos < nsk) {
             h = S.sk[pos];
             const uint32_t sw = S.sc[(uint32_t)h & (kSlots - 1)];
             const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);
-            first = true;
-            for (uint32_t q = a; q < e; ++q) {  // 2 <= m <= kSortMaxM
+            first = e - a <= kSortMaxM;
+            for (uint32_t q = first ? a : e; q < e; ++q) {  // 2 <= m <= kSortMaxM
                 if (q != pos && S.sk[q] == h) {
                     ++cnt;
                     first = first && q > pos;
@@ -1228,6 +1218,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         wb = (uint32_t)__shfl((int)wb, 0);
         if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
     }
+    if (nhot) lds_barrier();  // (uniform) the loop above has read sk before the crowded slots' marks
     // crowded slots (a key repeated more than kSortMaxM times hashes there), one
     // per wave: each round takes the first key not yet counted as the pivot, counts
     // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
