@@ -1205,10 +1205,17 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
             const uint32_t sw = S.sc[(uint32_t)h & (kSlots - 1)];
             const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);
             first = e - a <= kSortMaxM;
-            for (uint32_t q = first ? a : e; q < e; ++q) {  // 2 <= m <= kSortMaxM
-                if (q != pos && S.sk[q] == h) {
-                    ++cnt;
-                    first = first && q > pos;
+            if (first) {
+                // the slot's keys read all at once (2 <= m <= kSortMaxM; past the slot:
+                // this key's own position, excluded below), not one round trip each
+#pragma unroll
+                for (uint32_t t = 0; t < kSortMaxM; ++t) {
+                    const uint32_t q = a + t;
+                    const unsigned long long x = S.sk[q < e ? q : pos];
+                    if (q < e && q != pos && x == h) {
+                        ++cnt;
+                        first = first && q > pos;
+                    }
                 }
             }
         }

@@ -1,0 +1,98 @@
+"""Diagnostic (round 4): where K4s's time goes, per phase of sort_list.
+
+Builds lib/variants/libkmc_k4sprof.so from the current kmc_hash.hip with clock
+reads (s_memtime) patched in at the phase boundaries of sort_list (wave 0 of each
+workgroup, accumulated in registers over its lists, one device add per workgroup
+at the end) -- the product source carries none of it.  `--build` on the build host;
+on the GPU box (no flag) it runs C4 (scripts/cbench.py's GRCh38-like genome) through
+the variant and prints cycles per list and phase for the common and big instances.
+Wave 0's phase times include its waits at the barriers that end them."""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "dna-kmeres-parallel_amd")
+VLIB = os.path.join(PKG, "lib", "variants", "libkmc_k4sprof.so")
+PH = ["load+A", "rank+B", "scan+C1C2", "scatter", "D", "dedup+hot", "E"]
+
+
+def build():
+    src = open(os.path.join(PKG, "csrc", "kmc_hash.hip")).read()
+
+    def rep(a, b):
+        nonlocal src
+        assert src.count(a) == 1, a
+        src = src.replace(a, b)
+    rep("template <class C>\n__device__ __forceinline__ void sort_list(",
+        "__device__ unsigned long long g_k4s_prof[2][8];\n"
+        "#define TS(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); acc[i] += _t - tp; tp = _t; } while (0)\n"
+        "template <class C>\n__device__ __forceinline__ void sort_list(")
+    rep("uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0) {",
+        "uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0, unsigned long long (&acc)[8]) {\n"
+        "    unsigned long long tp = __builtin_amdgcn_s_memtime();\n    acc[7] += 1;")
+    rep("    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding\n",
+        "    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding\n    TS(0);\n")
+    rep("    lds_barrier();  // B: every key ranked\n", "    lds_barrier();  // B: every key ranked\n    TS(1);\n")
+    rep("    lds_barrier();  // C2: slot starts\n", "    lds_barrier();  // C2: slot starts\n    TS(2);\n")
+    rep("    lds_barrier();  // D: the keys of the failing slots sorted by slot\n",
+        "    TS(3);\n    lds_barrier();  // D: the keys of the failing slots sorted by slot\n    TS(4);\n")
+    rep("    lds_barrier();  // E: every key emitted\n", "    TS(5);\n    lds_barrier();  // E: every key emitted\n")
+    rep("    if (tid == 0) p.ndist[l] = S.out;\n}", "    if (tid == 0) p.ndist[l] = S.out;\n    TS(6);\n}")
+    rep("                           nb0, ne0);\n    }\n}",
+        "                           nb0, ne0, acc);\n    }\n"
+        "    if (threadIdx.x == 0) for (int i = 0; i < 8; ++i) atomicAdd(&g_k4s_prof[1][i], acc[i]);\n}")
+    rep("    const int64_t nl = (int64_t)*p.nbig;\n", "    const int64_t nl = (int64_t)*p.nbig;\n    unsigned long long acc[8] = {};\n")
+    rep("        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0);",
+        "        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0, acc);")
+    rep("    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n",
+        "    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n    unsigned long long acc[8] = {};\n")
+    rep("        b0 = nb0;\n        e0 = ne0;\n    }\n}",
+        "        b0 = nb0;\n        e0 = ne0;\n    }\n    if (threadIdx.x == 0) for (int i = 0; i < 8; ++i) atomicAdd(&g_k4s_prof[0][i], acc[i]);\n}")
+    src += ('\nextern "C" __attribute__((visibility("default"))) int kmc_k4sprof_read(unsigned long long *out) {\n'
+            '    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_k4s_prof), sizeof(kmc::g_k4s_prof)) != hipSuccess) return 1;\n'
+            '    static const unsigned long long z[16] = {};\n'
+            '    return hipMemcpyToSymbol(HIP_SYMBOL(kmc::g_k4s_prof), z, sizeof(z)) != hipSuccess;\n}\n')
+    os.makedirs(os.path.join(PKG, "build", "v"), exist_ok=True)
+    tmp = os.path.join(PKG, "build", "v", "kmc_hash_k4sprof.hip")
+    open(tmp, "w").write(src)
+    H = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-fvisibility=hidden", "-std=c++17",
+         "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc")]
+    obj = tmp[:-4] + ".o"
+    subprocess.check_call(H + ["-c", tmp, "-o", obj])
+    others = sorted(os.path.join(PKG, "build", f) for f in os.listdir(os.path.join(PKG, "build"))
+                    if f.startswith("kmc_") and f.endswith(".o") and f != "kmc_hash.o")
+    subprocess.check_call(H + ["-shared", "-o", VLIB, obj] + others +
+                          ["-Wl,--version-script=" + os.path.join(PKG, "libkmc.map"), "-L/opt/rocm/lib", "-lrccl",
+                           "-Wl,-rpath,/opt/rocm/lib"])
+    print("built", VLIB)
+
+
+def run():
+    os.environ["KMC_LIB"] = VLIB
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import torch
+    import kmc
+    import cbench
+    dev = torch.device("cuda:0")
+    data, idx, _ = cbench.grch38_like(torch, dev, 3.1)
+    lib = ctypes.CDLL(VLIB)
+    out = (ctypes.c_ulonglong * 16)()
+    for it in range(3):
+        r = kmc.count_canonical(data, idx, 31, flags=kmc.CANON_SOFTMASK)
+        torch.cuda.synchronize()
+        del r
+        assert lib.kmc_k4sprof_read(out) == 0
+    for inst, name in ((0, "common"), (1, "big")):
+        v = list(out[8 * inst:8 * inst + 8])
+        nl = v[7]
+        tot = sum(v[:7])
+        print("%s: %d lists, %.0f cycles per list (wave 0)" % (name, nl, tot / max(nl, 1)))
+        for i, ph in enumerate(PH):
+            print("   %-10s %8.0f cycles  %5.1f %%" % (ph, v[i] / max(nl, 1), 100.0 * v[i] / max(tot, 1)))
+
+
+if __name__ == "__main__":
+    build() if "--build" in sys.argv else run()
