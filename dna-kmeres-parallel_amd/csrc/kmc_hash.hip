@@ -431,12 +431,7 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
             a[i] = b + i < nbk ? cn[b + i] : 0u;
             t += a[i];
         }
-        uint32_t x = t;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
+        const uint32_t x = wave_incl_scan(t);
         uint32_t run = x - t;
 #pragma unroll
         for (int i = 0; i < kPerLane; ++i) {
@@ -1147,12 +1142,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         w[i] = run | (c << 16) | (dist ? kSlotDistinct : 0u);  // exclusive start, relative to the thread
         run += dist ? 0u : c;
     }
-    uint32_t incl = run;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-        if (lane >= d) incl += y;
-    }
+    const uint32_t incl = wave_incl_scan(run);
     if (lane == 63) S.wsum[wv] = incl;
     lds_barrier();  // C1: wave totals
     uint32_t base = incl - run, nsk = 0u;  // nsk: keys of the slots that failed the test
@@ -1187,7 +1177,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         if (am) {
             uint32_t wb = 0u;
             if (lane == 0) wb = atomicAdd(&S.out, (uint32_t)__popcll(am));
-            wb = (uint32_t)__shfl((int)wb, 0);
+            wb = __builtin_amdgcn_readlane(wb, 0);  // (a v_readlane, where __shfl is a ds_bpermute)
             if (alone) emit_pair(p, b0 + wb + (uint32_t)__popcll(am & lt), kh[j], 1u);
         }
     }
@@ -1222,7 +1212,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         const uint64_t m = __ballot(first);
         uint32_t wb = 0u;
         if (lane == 0 && m) wb = atomicAdd(&S.out, (uint32_t)__popcll(m));
-        wb = (uint32_t)__shfl((int)wb, 0);
+        wb = __builtin_amdgcn_readlane(wb, 0);
         if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
     }
     if (nhot) lds_barrier();  // (uniform) the loop above has read sk before the crowded slots' marks

@@ -125,14 +125,25 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
 }
 
+// Inclusive prefix sum over the wave's 64 lanes in six DPP adds (row_shr 1/2/4/8
+// within each row of 16, then row_bcast 15 and 31 carry the row totals up): VALU
+// only, where a __shfl_up ladder is six ds_bpermute round trips through the LDS.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
     return x;
 }
 
-// Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for
-// the wave's outstanding global loads, so the tile prefetch keeps streaming.
 // o[t] = x of lane t of this lane's quad (DPP quad_perm broadcasts: VALU, no LDS)
 __device__ __forceinline__ void quad_bcast4(uint32_t x, uint32_t *o) {
     o[0] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x00, 0xF, 0xF, false);
@@ -141,6 +152,8 @@ __device__ __forceinline__ void quad_bcast4(uint32_t x, uint32_t *o) {
     o[3] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xFF, 0xF, 0xF, false);
 }
 
+// Workgroup barrier ordering LDS only: unlike __syncthreads() it does not wait for
+// the wave's outstanding global loads, so the tile prefetch keeps streaming.
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
