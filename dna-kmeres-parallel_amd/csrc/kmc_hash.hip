@@ -1217,35 +1217,50 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     }
     if (nhot) lds_barrier();  // (uniform) the loop above has read sk before the crowded slots' marks
     // crowded slots (a key repeated more than kSortMaxM times hashes there), one
-    // per wave: each round takes the first key not yet counted as the pivot, counts
-    // its copies 64 at a time and marks them (kEmptyH): O(m) per distinct key
+    // per wave: each round counts the copies of a pivot key 128 at a time, marks
+    // them (kEmptyH) and finds the next pivot -- the first key left -- in the same
+    // pass: O(m) per distinct key.  Each lane keeps one of the slot's (key, count)
+    // results, emitted 64 at a time with one reservation.  (Round 4: the pivot
+    // search was a pass of its own, the pivot a ds_bpermute, and every distinct key
+    // its own reservation round trip.)
     for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kBlk / 64) {
         const uint32_t sw = S.sc[S.hot[hs]];
         const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);
-        uint32_t c = a;
+        uint32_t c = a, nd = 0u;  // nd: distinct keys found (wave-uniform)
+        unsigned long long piv = S.sk[a], myk = 0;  // (the same address in every lane: a broadcast)
+        uint32_t myc = 0u;
         for (;;) {
-            unsigned long long piv = kEmptyH;
-            for (; c < e; c += 64) {
-                const uint32_t q = c + (uint32_t)lane;
-                const unsigned long long x = q < e ? S.sk[q] : kEmptyH;
-                const uint64_t bal = __ballot(x != kEmptyH);
-                if (bal) {
-                    const int f = __builtin_ctzll(bal);
-                    piv = (unsigned long long)__shfl((long long)x, f);
-                    c += (uint32_t)f;
-                    break;
+            uint32_t cnt = 0u, nx = e;
+            for (uint32_t q0 = c; q0 < e; q0 += 128) {
+                const uint32_t q1 = q0 + (uint32_t)lane, q2 = q1 + 64u;
+                const unsigned long long x1 = q1 < e ? S.sk[q1] : kEmptyH;
+                const unsigned long long x2 = q2 < e ? S.sk[q2] : kEmptyH;
+                const bool e1 = x1 == piv, e2 = x2 == piv;
+                cnt += (uint32_t)__popcll(__ballot(e1)) + (uint32_t)__popcll(__ballot(e2));
+                if (e1) S.sk[q1] = kEmptyH;
+                if (e2) S.sk[q2] = kEmptyH;
+                if (nx == e) {  // (uniform) the first key of another value
+                    const uint64_t n1 = __ballot(!e1 && x1 != kEmptyH), n2 = __ballot(!e2 && x2 != kEmptyH);
+                    if (n1) nx = q0 + (uint32_t)__builtin_ctzll(n1);
+                    else if (n2) nx = q0 + 64u + (uint32_t)__builtin_ctzll(n2);
                 }
             }
-            if (c >= e) break;  // wave-uniform
-            uint32_t cnt = 0u;
-            for (uint32_t q0 = c; q0 < e; q0 += 64) {
-                const uint32_t q = q0 + (uint32_t)lane;
-                const bool eq = q < e && S.sk[q] == piv;
-                cnt += (uint32_t)__popcll(__ballot(eq));
-                if (eq) S.sk[q] = kEmptyH;
+            if (lane == (int)(nd & 63u)) {
+                myk = piv;
+                myc = cnt;
             }
-            if (lane == 0) emit_pair(p, b0 + atomicAdd(&S.out, 1u), piv, cnt);
-            ++c;
+            ++nd;
+            const bool last = nx >= e;
+            if ((nd & 63u) == 0u || last) {  // (uniform) this batch of results out
+                const uint32_t nb = ((nd - 1u) & 63u) + 1u;
+                uint32_t wb = 0u;
+                if (lane == 0) wb = atomicAdd(&S.out, nb);
+                wb = __builtin_amdgcn_readlane(wb, 0);
+                if ((uint32_t)lane < nb) emit_pair(p, b0 + wb + (uint32_t)lane, myk, myc);
+            }
+            if (last) break;
+            c = nx;
+            piv = S.sk[nx];  // (not marked: a value other than piv's)
         }
     }
     lds_barrier();  // E: every key emitted

@@ -4,7 +4,7 @@ Builds lib/variants/libkmc_k4sprof.so from the current kmc_hash.hip with clock
 reads (s_memtime) patched in at the phase boundaries of sort_list (wave 0 of each
 workgroup, accumulated in registers over its lists, one device add per workgroup
 at the end) -- the product source carries none of it.  `--build` on the build host;
-on the GPU box (no flag) it runs C4 (scripts/cbench.py's GRCh38-like genome) through
+on the GPU box (no flag) it runs C4 (scripts/cbench.py's GRCh38-like genome; --c4r: C4R's) through
 the variant and prints cycles per list and phase for the common and big instances.
 Wave 0's phase times include its waits at the barriers that end them."""
 import ctypes
@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "dna-kmeres-parallel_amd")
 VLIB = os.path.join(PKG, "lib", "variants", "libkmc_k4sprof.so")
-PH = ["load+A", "rank+B", "scan+C1C2", "scatter", "D", "dedup+hot", "E"]
+PH = ["load+A", "rank+B", "scan+C1C2", "scatter", "D", "pairwise", "E", "hot"]
 
 
 def build():
@@ -26,33 +26,34 @@ def build():
         assert src.count(a) == 1, a
         src = src.replace(a, b)
     rep("template <class C>\n__device__ __forceinline__ void sort_list(",
-        "__device__ unsigned long long g_k4s_prof[2][8];\n"
+        "__device__ unsigned long long g_k4s_prof[2][10];\n"
         "#define TS(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); acc[i] += _t - tp; tp = _t; } while (0)\n"
         "template <class C>\n__device__ __forceinline__ void sort_list(")
     rep("uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0) {",
-        "uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0, unsigned long long (&acc)[8]) {\n"
-        "    unsigned long long tp = __builtin_amdgcn_s_memtime();\n    acc[7] += 1;")
+        "uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0, unsigned long long (&acc)[10]) {\n"
+        "    unsigned long long tp = __builtin_amdgcn_s_memtime();\n    acc[9] += 1;")
     rep("    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding\n",
         "    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding\n    TS(0);\n")
     rep("    lds_barrier();  // B: every key ranked\n", "    lds_barrier();  // B: every key ranked\n    TS(1);\n")
     rep("    lds_barrier();  // C2: slot starts\n", "    lds_barrier();  // C2: slot starts\n    TS(2);\n")
     rep("    lds_barrier();  // D: the keys of the failing slots sorted by slot\n",
         "    TS(3);\n    lds_barrier();  // D: the keys of the failing slots sorted by slot\n    TS(4);\n")
-    rep("    lds_barrier();  // E: every key emitted\n", "    TS(5);\n    lds_barrier();  // E: every key emitted\n")
+    rep("    lds_barrier();  // E: every key emitted\n", "    TS(7);\n    lds_barrier();  // E: every key emitted\n")
+    rep("    if (nhot) lds_barrier();", "    TS(5);\n    if (nhot) lds_barrier();")
     rep("    if (tid == 0) p.ndist[l] = S.out;\n}", "    if (tid == 0) p.ndist[l] = S.out;\n    TS(6);\n}")
     rep("                           nb0, ne0);\n    }\n}",
         "                           nb0, ne0, acc);\n    }\n"
-        "    if (threadIdx.x == 0) for (int i = 0; i < 8; ++i) atomicAdd(&g_k4s_prof[1][i], acc[i]);\n}")
-    rep("    const int64_t nl = (int64_t)*p.nbig;\n", "    const int64_t nl = (int64_t)*p.nbig;\n    unsigned long long acc[8] = {};\n")
+        "    if (threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[1][i], acc[i]);\n}")
+    rep("    const int64_t nl = (int64_t)*p.nbig;\n", "    const int64_t nl = (int64_t)*p.nbig;\n    unsigned long long acc[10] = {};\n")
     rep("        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0);",
         "        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0, acc);")
     rep("    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n",
-        "    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n    unsigned long long acc[8] = {};\n")
+        "    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n    unsigned long long acc[10] = {};\n")
     rep("        b0 = nb0;\n        e0 = ne0;\n    }\n}",
-        "        b0 = nb0;\n        e0 = ne0;\n    }\n    if (threadIdx.x == 0) for (int i = 0; i < 8; ++i) atomicAdd(&g_k4s_prof[0][i], acc[i]);\n}")
+        "        b0 = nb0;\n        e0 = ne0;\n    }\n    if (threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[0][i], acc[i]);\n}")
     src += ('\nextern "C" __attribute__((visibility("default"))) int kmc_k4sprof_read(unsigned long long *out) {\n'
             '    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_k4s_prof), sizeof(kmc::g_k4s_prof)) != hipSuccess) return 1;\n'
-            '    static const unsigned long long z[16] = {};\n'
+            '    static const unsigned long long z[20] = {};\n'
             '    return hipMemcpyToSymbol(HIP_SYMBOL(kmc::g_k4s_prof), z, sizeof(z)) != hipSuccess;\n}\n')
     os.makedirs(os.path.join(PKG, "build", "v"), exist_ok=True)
     tmp = os.path.join(PKG, "build", "v", "kmc_hash_k4sprof.hip")
@@ -77,18 +78,22 @@ def run():
     import kmc
     import cbench
     dev = torch.device("cuda:0")
-    data, idx, _ = cbench.grch38_like(torch, dev, 3.1)
+    if "--c4r" in sys.argv:  # the repeat-rich genome of C4R
+        import genome_synth
+        data, idx, _, _ = genome_synth.repeat_genome(torch, dev, 3.1)
+    else:
+        data, idx, _ = cbench.grch38_like(torch, dev, 3.1)
     lib = ctypes.CDLL(VLIB)
-    out = (ctypes.c_ulonglong * 16)()
+    out = (ctypes.c_ulonglong * 20)()
     for it in range(3):
         r = kmc.count_canonical(data, idx, 31, flags=kmc.CANON_SOFTMASK)
         torch.cuda.synchronize()
         del r
         assert lib.kmc_k4sprof_read(out) == 0
     for inst, name in ((0, "common"), (1, "big")):
-        v = list(out[8 * inst:8 * inst + 8])
-        nl = v[7]
-        tot = sum(v[:7])
+        v = list(out[10 * inst:10 * inst + 10])
+        nl = v[9]
+        tot = sum(v[:8])
         print("%s: %d lists, %.0f cycles per list (wave 0)" % (name, nl, tot / max(nl, 1)))
         for i, ph in enumerate(PH):
             print("   %-10s %8.0f cycles  %5.1f %%" % (ph, v[i] / max(nl, 1), 100.0 * v[i] / max(tot, 1)))
