@@ -175,6 +175,53 @@ def test_canonical_crowded_list_deferred(kmc, oracle, cuda):
         assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "k=%d" % k)
 
 
+def _fmix62(h):
+    """fmix62 of kmc_hash.hip (uint64 arrays, wrapping multiplies)."""
+    m62 = np.uint64((1 << 62) - 1)
+    with np.errstate(over="ignore"):
+        h = h ^ (h >> np.uint64(31))
+        h = (h * np.uint64(0xFF51AFD7ED558CCD)) & m62
+        h = h ^ (h >> np.uint64(31))
+        h = (h * np.uint64(0xC4CEB9FE1A85EC53)) & m62
+        h = h ^ (h >> np.uint64(31))
+    return h
+
+
+@pytest.mark.parametrize("nd", [9, 64, 65, 100])
+def test_canonical_crowded_slot_many_keys(kmc, oracle, cuda, nd):
+    """A crowded K4s slot holding many distinct keys: nd distinct 31-mers whose
+    fmix62(canonical key) share the low 12 bits (one slot of the common instance's
+    4 096), each written 1-5 times between N's, in a record short enough to be one
+    list -- the crowded-slot rounds then find nd pivots in a slot of ~3 nd keys
+    (over 128 keys: several chunk pairs per pass), and emit their results 64 at a
+    time (64 / 65 / 100: one full batch, one more, a partial second), counts >= 4
+    through the count side array.  Records of random keys beside it."""
+    k = 31
+    rng = np.random.default_rng(900 + nd)
+    codes = rng.integers(0, 1 << 62, size=1 << 21, dtype=np.uint64)
+    rc = np.zeros_like(codes)
+    for q in range(k):  # reverse complement of the MSB-first 2-bit code
+        rc |= (np.uint64(3) - ((codes >> np.uint64(2 * q)) & np.uint64(3))) << np.uint64(2 * (k - 1 - q))
+    canon = np.minimum(codes, rc)
+    sel = np.flatnonzero((_fmix62(canon) & np.uint64(4095)) == 0)
+    _, first = np.unique(canon[sel], return_index=True)
+    pick = codes[sel[np.sort(first)][:nd]]
+    assert pick.size == nd
+    bases = np.frombuffer(b"ACGT", dtype=np.uint8)
+    parts = []
+    for i, c in enumerate(pick):
+        kmer = bases[[(int(c) >> (2 * (k - 1 - q))) & 3 for q in range(k)]]
+        for _ in range(i % 5 + 1):
+            parts += [kmer, np.frombuffer(b"N", dtype=np.uint8)]
+    rec = np.concatenate(parts + [np.zeros(1, np.uint8)])
+    data2, idx2 = random_records(rng, [5000, 300_000])
+    data = np.concatenate([rec, data2])
+    idx = np.concatenate([[0], rec.size + idx2]).astype(np.int64)
+    exp = oracle.count_canonical(data, idx, k)
+    assert int(exp[2][1] - exp[2][0]) == nd and exp[1][:nd].max() == 5
+    assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "nd=%d" % nd)
+
+
 def test_canonical_size_independent_properties(kmc, cuda):
     """64 Mbase: counts sum to the valid windows; canonical == forward folded by revcomp."""
     import torch
