@@ -222,6 +222,52 @@ def test_canonical_crowded_slot_many_keys(kmc, oracle, cuda, nd):
     assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "nd=%d" % nd)
 
 
+def test_canonical_slot_distinctness_test_edges(kmc, oracle, cuda):
+    """K4s proves a slot's keys distinct when the high half of its word -- one
+    2^sub per key, sub = bits 12-15 of fmix62(key) -- has as many bits set as the
+    slot has keys.  Constructed edges, each group in a slot of its own of one
+    list: 16 distinct keys on all 16 subs (the largest slot that passes); 2
+    distinct keys on sub 15 (the sum carries out of the word: fails, pairwise
+    check); 9 keys on 9 subs, one of them written twice (fails, crowded); 8 keys,
+    two on one sub (fails, pairwise).  Counts against the oracle."""
+    k = 31
+    rng = np.random.default_rng(4242)
+    codes = rng.integers(0, 1 << 62, size=1 << 22, dtype=np.uint64)
+    rc = np.zeros_like(codes)
+    for q in range(k):
+        rc |= (np.uint64(3) - ((codes >> np.uint64(2 * q)) & np.uint64(3))) << np.uint64(2 * (k - 1 - q))
+    canon = np.minimum(codes, rc)
+    h = _fmix62(canon)
+    slot = (h & np.uint64(4095)).astype(np.int64)
+    sub = ((h >> np.uint64(12)) & np.uint64(15)).astype(np.int64)
+
+    def keys_of(sl, subs):  # one forward code per requested sub (distinct canonical keys)
+        out, seen = [], set()
+        for su in subs:
+            i = np.flatnonzero((slot == sl) & (sub == su) & ~np.isin(canon, list(seen) or [np.uint64(0)]))
+            assert i.size, (sl, su)
+            seen.add(canon[i[0]])
+            out.append(codes[i[0]])
+        return out
+    groups = [(keys_of(7, range(16)), [1] * 16),
+              (keys_of(8, [15, 15]), [1, 1]),
+              (keys_of(9, range(9)), [2] + [1] * 8),
+              (keys_of(10, [3, 3, 0, 1, 2, 4, 5, 6]), [1] * 8)]
+    bases = np.frombuffer(b"ACGT", dtype=np.uint8)
+    parts = []
+    for ks, reps in groups:
+        for c, r in zip(ks, reps):
+            kmer = bases[[(int(c) >> (2 * (k - 1 - q))) & 3 for q in range(k)]]
+            parts += [kmer, np.frombuffer(b"N", dtype=np.uint8)] * r
+    rec = np.concatenate(parts + [np.zeros(1, np.uint8)])
+    data2, idx2 = random_records(rng, [2000])
+    data = np.concatenate([rec, data2])
+    idx = np.concatenate([[0], rec.size + idx2]).astype(np.int64)
+    exp = oracle.count_canonical(data, idx, k)
+    assert int(exp[2][1]) == 16 + 2 + 9 + 8
+    assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "slot edges")
+
+
 def test_canonical_size_independent_properties(kmc, cuda):
     """64 Mbase: counts sum to the valid windows; canonical == forward folded by revcomp."""
     import torch
