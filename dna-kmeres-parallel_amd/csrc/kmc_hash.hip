@@ -1004,9 +1004,9 @@ constexpr uint32_t kHotMax = 128;                     // crowded slots per list 
 
 template <class C>
 struct K4sLds {
-    unsigned long long sk[C::kCap];   // the list, sorted by slot
+    unsigned long long sk[C::kCap];   // the keys of the slots that fail the distinctness test, sorted by slot
     uint32_t sc[C::kSlots];           // slot words: count | sub-hash sum, then start | count | distinct
-    uint32_t hot[kHotMax];            // slots holding more than kSortMaxM keys
+    uint32_t hot[kHotMax];            // failing slots holding more than kSortMaxM keys (crowded)
     uint32_t wsum[C::kBlock / 64];
     uint32_t pfs[64];                 // scratch target of the next list's L2 prefetch (never read)
     uint32_t out;                     // distinct keys emitted
