@@ -472,6 +472,11 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
 // taking more than RING - 7 of a round's entries: skewed input) go straight to
 // their position in a cold path.  nbk = 2^lgb <= kMaxBk.
 constexpr int kRingEnt = 16384;  // 8-byte ring entries in LDS (128 KB)
+#ifndef KMC_K3B_SEG
+#define KMC_K3B_SEG 16
+#endif
+constexpr uint32_t kSeg = KMC_K3B_SEG;  // entries per HBM segment: 8 (64 bytes) or 16 (a whole 128-byte line)
+static_assert(kSeg == 8 || kSeg == 16, "K3b segments");
 struct Ring8Lds {
     unsigned long long ring[kRingEnt];
     uint32_t W[2][kMaxBk];
@@ -490,9 +495,9 @@ struct Ring8 {
     __device__ __forceinline__ uint32_t rmask() const { return (1u << rlg) - 1u; }
     __device__ __forceinline__ uint32_t bucket_of_thread() const { return threadIdx.x >> (10 - lgb); }
     __device__ __forceinline__ uint32_t member() const { return threadIdx.x & ((1u << (10 - lgb)) - 1u); }
-    __device__ __forceinline__ uint32_t rot(uint32_t b) const { return (8u * (b & 3u)) & rmask(); }
+    __device__ __forceinline__ uint32_t rot(uint32_t b) const { return (kSeg * (b & 3u)) & rmask(); }
     __device__ __forceinline__ uint32_t word(uint32_t b, unsigned long long f) const {
-        const uint32_t f0 = (uint32_t)f & 7u;
+        const uint32_t f0 = (uint32_t)f & (kSeg - 1u);
         const uint32_t half = ((uint32_t)f - f0 + rot(b)) & rmask();
         return (((b << rlg) + half) << 16) | f0;
     }
@@ -509,7 +514,7 @@ struct Ring8 {
         if (member() == 0) {
             const uint32_t b = bucket_of_thread();
             L->W[0][b] = word(b, f0);
-            L->gH[b] = f0 & ~7ull;
+            L->gH[b] = f0 & ~(unsigned long long)(kSeg - 1u);
         }
     }
     // Phase A: entries val[j] (bit j of vm) to buckets bk[j].
@@ -552,44 +557,49 @@ struct Ring8 {
     // about half the HBM write rate: scripts/write_microbench.hip).
     __device__ __forceinline__ void flush() {
         const uint32_t b = bucket_of_thread(), j = member(), tpb = 1u << (10 - lgb);
-        const uint32_t f0 = (uint32_t)F & 7u;
+        const uint32_t f0 = (uint32_t)F & (kSeg - 1u);
         const uint32_t n = (L->W[par][b] & 0xFFFFu) - f0;
         const unsigned long long F1 = F + n, H = F - f0;
         const uint32_t R = 1u << rlg;
         const unsigned long long top = F1 < H + R ? F1 : H + R;
-        const uint32_t nseg = (uint32_t)((top - H) >> 3);
+        const uint32_t nseg = (uint32_t)((top - H) / kSeg);
         const uint32_t rt = rot(b);
         const uint32_t q = threadIdx.x & 3u;
         const uint4 *ring4 = reinterpret_cast<const uint4 *>(&L->ring[0]);  // 2 entries per uint4
         for (uint32_t i = j; __any(i < nseg); i += tpb) {  // (wave-uniform trip count: the quads need every lane)
-            const unsigned long long g0 = H + 8ull * i;
+            const unsigned long long g0 = H + (unsigned long long)kSeg * i;
             const bool seg = i < nseg;
             if (seg && g0 < V) {  // partly before V (a piece start after an overflow): entry by entry
-                for (uint32_t e = 0; e < 8; ++e)
+                for (uint32_t e = 0; e < kSeg; ++e)
                     if (g0 + e >= V) dst[g0 + e] = L->ring[(b << rlg) + (((uint32_t)(g0 + e) + rt) & rmask())];
             }
             // this lane's segment: uint4 index of its chunk 0 in the ring (bit 31: a
             // whole segment to store) and its list position / 8
             const uint32_t c0 = ((b << rlg) + (((uint32_t)g0 + rt) & rmask())) >> 1;
             const uint32_t A = c0 | (seg && g0 >= V ? 0x80000000u : 0u);
-            const uint64_t gs = g0 >> 3;
+            const uint64_t gs = g0 / kSeg;
             uint32_t a[4], glo[4], ghi[4];
             quad_bcast4(A, a);
             quad_bcast4((uint32_t)gs, glo);
             quad_bcast4((uint32_t)(gs >> 32), ghi);
-            uint4 v[4];
+            // 16-byte pieces q (and q + 4 for 16-entry segments) of each lane's segment
 #pragma unroll
-            for (int t = 0; t < 4; ++t) v[t] = ring4[(a[t] & 0x7FFFFFFFu) + q];  // (a quad without a segment reads harmlessly)
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (a[t] & 0x80000000u)
-                    reinterpret_cast<uint4 *>(dst + 8ull * ((uint64_t)glo[t] | ((uint64_t)ghi[t] << 32)))[q] = v[t];
+            for (int t = 0; t < 4; ++t) {
+                const uint32_t at = a[t];
+                const uint4 v0 = ring4[(at & 0x7FFFFFFFu) + q];  // (a quad without a segment reads harmlessly)
+                const uint4 v1 = kSeg == 16 ? ring4[(at & 0x7FFFFFFFu) + 4 + q] : v0;
+                if (at & 0x80000000u) {
+                    uint4 *sd = reinterpret_cast<uint4 *>(dst + kSeg * ((uint64_t)glo[t] | ((uint64_t)ghi[t] << 32)));
+                    sd[q] = v0;
+                    if (kSeg == 16) sd[4 + q] = v1;
+                }
+            }
         }
         if (F1 > H + R) V = F1;  // [H + R, F1) went straight to dst
         F = F1;
         if (j == 0) {
             L->W[par ^ 1u][b] = word(b, F1);
-            L->gH[b] = F1 & ~7ull;
+            L->gH[b] = F1 & ~(unsigned long long)(kSeg - 1u);
         }
         par ^= 1u;
     }
@@ -601,7 +611,7 @@ struct Ring8 {
     // End of a piece: the partial segment left in each ring, entry by entry.
     __device__ __forceinline__ void finish() {
         const uint32_t b = bucket_of_thread(), j = member(), tpb = 1u << (10 - lgb);
-        const unsigned long long H = F & ~7ull, lo = H > V ? H : V;
+        const unsigned long long H = F & ~(unsigned long long)(kSeg - 1u), lo = H > V ? H : V;
         const uint32_t rt = rot(b);
         for (unsigned long long g = lo + j; g < F; g += tpb)
             dst[g] = L->ring[(b << rlg) + (((uint32_t)g + rt) & rmask())];
