@@ -251,3 +251,72 @@ int64_t oracle_count_canonical(const uint8_t *data, const int64_t *indices, int6
     }
     return total;
 }
+
+/*
+ * Full-size digest of canonical counting (the config-scale check of
+ * kmc_count_canonical_hash, BASELINE configs[3]: 3.1 Gbase at k = 31, where the
+ * sort of oracle_count_canonical would need the whole key set in memory).  Same
+ * definition as oracle_count_canonical, restated as one rolling pass over ONE
+ * record (rec[0 .. E-1), E = entry length incl. terminator; windows i < E - k):
+ * the forward key shifts a base in at the bottom, the reverse complement's key
+ * shifts the complemented base in at the top, a run counter tracks validity.
+ *   *valid  = valid windows of the record
+ *   *digest = sum over valid windows of dg_hash(canonical key), mod 2^64
+ *             (= sum over the distinct keys of dg_hash(key) * count: any missing,
+ *             substituted or miscounted key changes it)
+ *   keys/counts = the distinct canonical keys with (dg_hash(key) >> sel_shift) ==
+ *             sel_val and their counts, sorted ascending (a subset compared key by
+ *             key with the GPU output restricted to the same predicate)
+ * dg_hash is splitmix64's finaliser, unrelated to the GPU's partition multiply and
+ * fmix62 list values (kmc_hash.hip), so the selected subset spans every list.
+ * Returns the number of selected distinct keys, or -1 when more than `cap`
+ * selected windows occur.
+ */
+uint64_t oracle_dg_hash(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int64_t oracle_canonical_digest(const uint8_t *rec, int64_t E, int k, int soft, int forward, int sel_shift,
+                                uint64_t sel_val, uint64_t *valid, uint64_t *digest, uint64_t *keys,
+                                uint32_t *counts, int64_t cap) {
+    const uint64_t mask = k == 32 ? ~0ull : (1ull << (2 * k)) - 1;
+    const int top = 2 * (k - 1);
+    uint64_t fw = 0, rc = 0, nv = 0, dg = 0;
+    int64_t m = 0;
+    int run = 0;
+    for (int64_t i = 0; i + 1 < E; ++i) { /* window ending at i starts at i - k + 1 <= E - k - 1 */
+        int c = canon_base_code(rec[i], soft);
+        if (c < 0) {
+            run = 0;
+            continue;
+        }
+        fw = ((fw << 2) | (uint64_t)c) & mask;
+        rc = (rc >> 2) | ((uint64_t)(3 - c) << top);
+        if (++run < k) continue;
+        const uint64_t key = (forward || fw < rc) ? fw : rc;
+        const uint64_t h = oracle_dg_hash(key);
+        ++nv;
+        dg += h;
+        if (sel_shift >= 64 || (h >> sel_shift) == sel_val) { /* 64: every key */
+            if (m >= cap) return -1;
+            keys[m++] = key;
+        }
+    }
+    *valid = nv;
+    *digest = dg;
+    qsort(keys, (size_t)m, sizeof(uint64_t), cmp_u64);
+    int64_t d = 0;
+    for (int64_t i = 0; i < m;) {
+        int64_t j = i;
+        while (j < m && keys[j] == keys[i]) ++j;
+        keys[d] = keys[i];
+        counts[d] = (uint32_t)(j - i);
+        ++d;
+        i = j;
+    }
+    return d;
+}

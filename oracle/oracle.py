@@ -50,6 +50,11 @@ def lib():
         L.oracle_count_canonical.restype = _I64
         L.oracle_count_canonical.argtypes = [_P, _P, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.oracle_min_kmeres2_row.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
+        L.oracle_dg_hash.restype = ctypes.c_uint64
+        L.oracle_dg_hash.argtypes = [ctypes.c_uint64]
+        L.oracle_canonical_digest.restype = _I64
+        L.oracle_canonical_digest.argtypes = [_P, _I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_uint64, _P, _P, _P, _P, _I64]
         _lib = L
     return _lib
 
@@ -97,6 +102,53 @@ def count_canonical(data, indices, k, soft=False, forward=False):
     tot = lib().oracle_count_canonical(dptr, _ptr(indices), n, k, int(soft), int(forward),
                                        _ptr(keys), _ptr(counts), _ptr(off))
     return keys[:tot], counts[:tot], off
+
+
+DIGEST_SEL_BITS = 12  # the selected subset: top 12 bits of dg_hash(key) == sel_val (1 key in 4 096)
+
+
+def canonical_digest(data, indices, k, soft=False, forward=False, sel_val=0, sel_bits=DIGEST_SEL_BITS,
+                     threads=16):
+    """oracle_canonical_digest over every record (records in parallel: ctypes drops
+    the GIL).  Returns a list of per-record dicts {valid, digest (uint64 as int),
+    keys (uint64, sorted), counts (uint32)}: the full-size check of the canonical
+    path (tests/test_canonical_full_size_gpu.py)."""
+    from concurrent.futures import ThreadPoolExecutor
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    indices = np.ascontiguousarray(indices, dtype=np.int64)
+    n = indices.size - 1
+    shift = 64 - sel_bits
+    base = data.ctypes.data
+
+    def one(s):
+        a, E = int(indices[s]), int(indices[s + 1] - indices[s])
+        cap = max(E // (1 << sel_bits) * 2 + 4096, 1)
+        while True:
+            keys = np.zeros(cap, dtype=np.uint64)
+            counts = np.zeros(cap, dtype=np.uint32)
+            nv, dg = ctypes.c_uint64(0), ctypes.c_uint64(0)
+            d = lib().oracle_canonical_digest(ctypes.c_void_p(base + a) if E else None, E, k, int(soft),
+                                              int(forward), shift, sel_val, ctypes.byref(nv), ctypes.byref(dg),
+                                              _ptr(keys), _ptr(counts), cap)
+            if d >= 0:
+                return {"valid": nv.value, "digest": dg.value, "keys": keys[:d], "counts": counts[:d]}
+            cap *= 4
+
+    order = sorted(range(n), key=lambda s: -int(indices[s + 1] - indices[s]))  # longest first
+    with ThreadPoolExecutor(max(1, min(threads, n))) as ex:
+        res = dict(zip(order, ex.map(one, order)))
+    return [res[s] for s in range(n)]
+
+
+def dg_hash(x):
+    """oracle_dg_hash on a numpy uint64 array (splitmix64's finaliser)."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(30))
+        x = x * np.uint64(0xBF58476D1CE4E5B9)
+        x = x ^ (x >> np.uint64(27))
+        x = x * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
 
 
 def min_kmeres2_row(sum_, indexes, cur, k, out=None):
@@ -196,6 +248,7 @@ def have_ref_kernel():
 def ref_kernel():
     global _ref_kernel
     if _ref_kernel is None:
+        import torch  # noqa: F401  (one HIP runtime per process: torch's, see kmc._load)
         L = ctypes.CDLL(os.path.join(REF_DIR, "libref_kernel.so"))
         L.ref_kernel_launch.argtypes = [_P, _P, ctypes.c_uint, _P]
         L.ref_min_kmeres2_launch.argtypes = [_P, _P, ctypes.c_int, ctypes.c_int, _P]

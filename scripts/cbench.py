@@ -18,38 +18,6 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def grch38_like(torch, dev, gbases, seed=38):
-    """Synthetic stand-in for GRCh38 (not in the container): chromosome-like
-    record lengths, uniform bases, N runs and lowercase runs."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    # relative sizes of chr1..22, X, Y, M-ish
-    rel = [248, 242, 198, 190, 181, 171, 159, 145, 138, 134, 135, 133, 114, 107, 102, 90, 83, 80, 59, 64, 47, 51,
-           156, 57, 1]
-    tot = sum(rel)
-    lens = [max(1000, int(gbases * 1e9 * r / tot)) for r in rel]
-    n = len(lens)
-    nbytes = sum(L + 1 for L in lens)
-    data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
-    chunk = 1 << 28
-    for o in range(0, nbytes, chunk):
-        m = min(chunk, nbytes - o)
-        data[o:o + m] = lut[torch.randint(0, 4, (m,), device=dev, generator=g, dtype=torch.int64).to(torch.uint8).long()]
-        # runs of 4096 bases: ~50 % lowercase, ~5 % N
-        r = torch.rand((m + 4095) // 4096, device=dev, generator=g)
-        run = r.repeat_interleave(4096)[:m]
-        seg = data[o:o + m]
-        seg[run < 0.5] += 32
-        seg[run > 0.95] = ord("N")
-    off = [0]
-    for L in lens:
-        off.append(off[-1] + L + 1)
-    offs = torch.tensor(off, dtype=torch.int64)
-    data[offs[1:] - 1] = 0
-    return data, offs.to(dev), lens
-
-
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -341,7 +309,8 @@ def main():
         torch.cuda.empty_cache()
     for cfg in [c for c in cfgs if c in ("c4", "c4r")]:
         if cfg == "c4":
-            data, idx, lens = grch38_like(torch, dev, a.gbases_c4)
+            import genome_synth
+            data, idx, lens = genome_synth.grch38_like(torch, dev, a.gbases_c4)
             extra = {"input": "iid ACGT, 5 % N runs, 50 % soft-masked runs (no repeats)"}
         else:  # repeat-rich stand-in (scripts/genome_synth.py)
             import genome_synth

@@ -20,7 +20,7 @@ table's add for an already-claimed key, hot keys in a pass, long lists.
 """
 import numpy as np
 
-# relative sizes of chr1..22, X, Y, M-ish (as scripts/cbench.py grch38_like)
+# relative sizes of chr1..22, X, Y, M-ish (both genomes below)
 REL = [248, 242, 198, 190, 181, 171, 159, 145, 138, 134, 135, 133, 114, 107, 102, 90, 83, 80, 59, 64, 47, 51,
        156, 57, 1]
 
@@ -136,3 +136,33 @@ def repeat_genome(torch, dev, gbases, seed=38, families=3000, min_len=1000):
         off += L + 1
     idx = np.concatenate([[0], np.cumsum([L + 1 for L in lens])]).astype(np.int64)
     return data, torch.from_numpy(idx).to(dev), lens, stats
+
+
+def grch38_like(torch, dev, gbases, seed=38):
+    """Synthetic stand-in for GRCh38 (not in the container): chromosome-like
+    record lengths, uniform bases, N runs and lowercase runs."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    rel = REL
+    tot = sum(rel)
+    lens = [max(1000, int(gbases * 1e9 * r / tot)) for r in rel]
+    n = len(lens)
+    nbytes = sum(L + 1 for L in lens)
+    data = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    lut = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    chunk = 1 << 28
+    for o in range(0, nbytes, chunk):
+        m = min(chunk, nbytes - o)
+        data[o:o + m] = lut[torch.randint(0, 4, (m,), device=dev, generator=g, dtype=torch.int64).to(torch.uint8).long()]
+        # runs of 4096 bases: ~50 % lowercase, ~5 % N
+        r = torch.rand((m + 4095) // 4096, device=dev, generator=g)
+        run = r.repeat_interleave(4096)[:m]
+        seg = data[o:o + m]
+        seg[run < 0.5] += 32
+        seg[run > 0.95] = ord("N")
+    off = [0]
+    for L in lens:
+        off.append(off[-1] + L + 1)
+    offs = torch.tensor(off, dtype=torch.int64)
+    data[offs[1:] - 1] = 0
+    return data, offs.to(dev), lens

@@ -76,13 +76,12 @@ def run():
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import torch
     import kmc
-    import cbench
+    import genome_synth
     dev = torch.device("cuda:0")
     if "--c4r" in sys.argv:  # the repeat-rich genome of C4R
-        import genome_synth
         data, idx, _, _ = genome_synth.repeat_genome(torch, dev, 3.1)
     else:
-        data, idx, _ = cbench.grch38_like(torch, dev, 3.1)
+        data, idx, _ = genome_synth.grch38_like(torch, dev, 3.1)
     lib = ctypes.CDLL(VLIB)
     out = (ctypes.c_ulonglong * 20)()
     for it in range(3):

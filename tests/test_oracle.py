@@ -254,3 +254,38 @@ def test_canonical_oracle_matches_python_strings(oracle, k):
             for key, c in py_canonical(bytes(recs[s]), k, soft).items():
                 exp[(s, key)] = c
         assert got == exp
+
+
+@pytest.mark.parametrize("k", [1, 5, 16, 21, 31])
+@pytest.mark.parametrize("sel_bits", [0, 3, 12])
+def test_canonical_digest_matches_sort_oracle(oracle, k, sel_bits):
+    """oracle_canonical_digest (the rolling, per-record restatement behind the
+    full-size canonical check) against oracle_count_canonical (sort + run-length):
+    valid windows, the sum of dg_hash(key) * count mod 2^64, and the selected
+    subset (top sel_bits of dg_hash(key) == sel_val; 0 bits: every key), on ragged
+    records with N runs, lowercase, '\\0' bytes inside a record, repeats."""
+    rng = np.random.default_rng(31 * k + sel_bits)
+    recs = []
+    for L in (0, 1, k - 1, k, k + 1, 200, 5000, 40_000):
+        s = rng.choice(np.frombuffer(b"ACGTNacgt\0", dtype=np.uint8), size=max(L, 0),
+                       p=[.22, .22, .22, .22, .02, .02, .025, .025, .025, .005])
+        recs.append(np.append(s, np.uint8(0)))
+    rep = np.frombuffer(b"ACGTTGCAAT" * 300 + b"tttt" * 200, dtype=np.uint8)
+    recs.append(np.append(rep, np.uint8(0)))
+    data = np.concatenate(recs)
+    idx = np.concatenate([[0], np.cumsum([r.size for r in recs])]).astype(np.int64)
+    M = (1 << 64) - 1
+    for soft, forward in ((False, False), (True, False), (True, True)):
+        keys, counts, off = oracle.count_canonical(data, idx, k, soft=soft, forward=forward)
+        h = oracle.dg_hash(keys)
+        for sel_val in ((0, 5) if sel_bits else (0,)):
+            res = oracle.canonical_digest(data, idx, k, soft=soft, forward=forward, sel_val=sel_val,
+                                          sel_bits=sel_bits, threads=4)
+            for s in range(idx.size - 1):
+                a, b = int(off[s]), int(off[s + 1])
+                r = res[s]
+                assert r["valid"] == int(counts[a:b].astype(np.int64).sum())
+                assert r["digest"] == sum(int(x) * int(c) for x, c in zip(h[a:b], counts[a:b])) & M
+                sel = (h[a:b] >> np.uint64(64 - sel_bits)) == np.uint64(sel_val) if sel_bits else slice(None)
+                np.testing.assert_array_equal(r["keys"], keys[a:b][sel])
+                np.testing.assert_array_equal(r["counts"], counts[a:b][sel])
