@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may run on")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_dense_k8_shards.json"),
                     help="HBM traffic per launch measured by rocprofv3 --pmc, per shard size (see profiles/)")
+    ap.add_argument("--pmc-lds", default=os.path.join(REPO, "profiles", "pmc_lds_k8_10gbase.json"),
+                    help="LDS-array cycles per window of the k = 8 kernel (rocprofv3 --pmc, see profiles/)")
     ap.add_argument("--allreduce-reps", type=int, default=20,
                     help="N > 1: all-reduces timed alone after the timed region")
     ap.add_argument("--reserve-cus", type=int, default=-1,
@@ -447,6 +449,19 @@ def pmc_traffic(path, k, data_bytes):
     return None
 
 
+def lds_floor(path, k):
+    """The LDS-array roof of the k = 8 histogram (7 array cycles per
+    wave-wide ds_add_u32, 72 % of them bank conflicts of random bins): the share of
+    the kernel's shader cycles in which an average CU's LDS array is busy
+    (SQ_LDS_IDX_ACTIVE / CUs / (GRBM_GUI_ACTIVE / 8), rocprofv3 PMC of this bench
+    command, profiles/pmc_lds_k8_10gbase.json).  None when not measured."""
+    if k != 8 or not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        m = json.load(f)
+    return m if m.get("k") == k and "lds_busy_frac" in m else None
+
+
 def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed, kern_ms, alg_bytes, timer):
     """Everything after the timed region, at every N: the all-reduce timed alone,
     the max-over-ranks statistics, the reference CPU path on rank 0, and the JSON
@@ -526,6 +541,21 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
                    if world > 1 else "none (1 GPU)",
         },
     }
+    # the roof that binds k = 8: the LDS array, not HBM
+    m = lds_floor(getattr(args, "pmc_lds", None), k)
+    if m is not None:
+        result["roofline"].update({
+            "binding": "lds",
+            "lds_floor_ms": m["lds_busy_frac"] * kern_ms,
+            "lds_floor_frac": m["lds_busy_frac"],
+            "lds_how": "the k = 8 kernel is bound by its LDS array, not HBM: an average CU's array is busy "
+                       "lds_floor_frac of the kernel's shader cycles (%.2f array cycles per wave-wide ds_add_u32, "
+                       "%.0f %% of them bank-conflict cycles of random bins; SQ_LDS_IDX_ACTIVE / %d CUs / "
+                       "(GRBM_GUI_ACTIVE / 8) over %d launches of the N = 1 bench command, %s); lds_floor_ms = that share "
+                       "of kernel_ms, the time of the LDS work alone"
+                       % (m["array_cycles_per_atomic"], 100 * m["conflict_frac"], m["cus"], m["launches"],
+                          os.path.relpath(args.pmc_lds, REPO)),
+        })
     if world > 1:
         dist.barrier()  # every rank's GPU work is done before rank 0 takes the host cores
     if rank == 0 and args.cpu_sample >= 0:

@@ -8,13 +8,14 @@ extern "C" const char *kmc_error_string(int code) {
         case KMC_OK: return "success";
         case KMC_ERR_INVALID_ARG: return "invalid argument";
         case KMC_ERR_UNSUPPORTED_K: return "k outside the supported range of this entry point";
-        case KMC_ERR_ALIGNMENT: return "data pointer must be 16-byte aligned";
+        case KMC_ERR_ALIGNMENT: return "pointer not aligned as required (data: 16 bytes, workspace: 256 bytes)";
         case KMC_ERR_WORKSPACE: return "workspace smaller than the required size";
         case KMC_ERR_IO: return "file cannot be opened or read";
         case KMC_ERR_NOMEM: return "allocation failed";
         case KMC_ERR_RCCL: return "RCCL call failed";
         case KMC_ERR_NO_DEVICE: return "no HIP device visible";
         case KMC_ERR_CAPACITY: return "output capacity smaller than the result";
+        case KMC_ERR_RECORD_TOO_LONG: return "a record has 2^31 or more windows in one call: int32 counts could wrap";
         default: return hipGetErrorString(static_cast<hipError_t>(code));
     }
 }

@@ -80,8 +80,15 @@ struct Params {
     Spill *spill;            // [G][spill_cap]
     uint32_t *spill_cnt;     // [G]
     uint32_t spill_cap;
-    uint32_t *status;        // host-mapped flag (kmc_dense_status): a workgroup overflowed its spill list
+    uint32_t *status;        // the call's status word (kmc_dense_args::status, or the device's host-mapped
+                             // kmc_dense_status flag): a kmc_status code when the counts are not valid
 };
+
+// Store a kmc_status code in the call's status word (a plain system-scope store:
+// the word may be host-mapped; any nonzero code marks the call failed).
+__device__ __forceinline__ void raise_status(uint32_t *st, uint32_t code) {
+    if (st) __hip_atomic_store(st, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // 1 or 0x10000 from bit `hb` (0/1): one v_mad_u32_u24 (hipcc otherwise emits
 // and + cmp + cndmask for the same select).
@@ -471,8 +478,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             p.spill_cnt[w] = (tb < te) ? misc[0] : 0u;
             // never expected (spill_cap_for bounds the entries), but a lost entry
             // would be a silent short count: raise the deferred status flag
-            if (tb < te && misc[0] > p.spill_cap && p.status)
-                __hip_atomic_store(p.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tb < te && misc[0] > p.spill_cap) raise_status(p.status, KMC_ERR_CAPACITY);
         }
     }
 }
@@ -530,6 +536,9 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     for (int64_t s = blockIdx.y; s < p.n; s += gridDim.y) {
         int64_t ca, ce;
         record_windows<K, Idx>(p, g, s, ca, ce);
+        // int32 bins (and invalid counts) of a record with >= 2^31 windows in range
+        // could wrap (the reference's int counters, main.cu:637, never see one)
+        if (blockIdx.x == 0 && tid == 0 && ce - ca >= ((int64_t)1 << 31)) raise_status(p.status, KMC_ERR_RECORD_TOO_LONG);
         if (ce <= ca) {
             for (int i = tid; i < RW * NH; i += 256) {
                 const int64_t c = c0 + i % RW + (i / RW) * NW;
@@ -697,7 +706,8 @@ int grid_size(int device, int &G) {
     return 0;
 }
 
-// The device's kmc_dense_status flag: host-mapped, written by the k = 8 kernel.
+// The device's kmc_dense_status flag: host-mapped, written by the dense kernels of
+// the calls that pass no status word of their own.
 int status_flag(int device, uint32_t **host, uint32_t **dev) {
     std::lock_guard<std::mutex> lk(g_mu);
     if ((int)g_dev.size() <= device) g_dev.resize(device + 1);
@@ -730,7 +740,7 @@ int take_status(int device) {
     }
     if (!h) return KMC_OK;
     const uint32_t v = __atomic_exchange_n(h, 0u, __ATOMIC_ACQ_REL);
-    return v ? KMC_ERR_CAPACITY : KMC_OK;
+    return (int)v;  // the code a kernel stored, KMC_OK if none
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -839,6 +849,7 @@ struct Request {
     int64_t wl, wh, rl, rh;
     void *ws;
     size_t ws_bytes;
+    uint32_t *status;        // the call's status word (NULL: the device's flag)
 };
 
 template <int K, class Idx>
@@ -890,8 +901,8 @@ int run_dense(const Request &q, hipStream_t st) {
     p.slab = reinterpret_cast<uint32_t *>(base + pl.L.slab);
     p.spill = Cfg<K>::P16 ? reinterpret_cast<Spill *>(base + pl.L.spill) : nullptr;
     p.spill_cap = pl.spill_cap;
-    p.status = nullptr;
-    if (Cfg<K>::P16) {
+    p.status = q.status;
+    if (!p.status) {
         uint32_t *sh = nullptr;
         e = status_flag(device, &sh, &p.status);
         if (e) return e;
@@ -1011,8 +1022,6 @@ extern "C" int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, un
     q.sum = sum;
     q.ld = num_seqs;
     q.derive = true;
-    int device = 0;
-    if (hipGetDevice(&device) == hipSuccess && take_status(device) != KMC_OK) return KMC_ERR_CAPACITY;
     return dispatch<int>(KMC_DROPIN_K, q, stream);
 }
 
@@ -1050,13 +1059,18 @@ extern "C" int kmc_count_dense_ex(const kmc_dense_args *a0, hipStream_t stream) 
     if (!a0->data || !a0->indices || !a0->sum) return KMC_ERR_INVALID_ARG;
     if (a0->read_hi < a0->read_lo || a0->win_hi < a0->win_lo) return KMC_ERR_INVALID_ARG;
     if (a0->sum_ld != 0 && a0->sum_ld < a0->num_seqs) return KMC_ERR_INVALID_ARG;
-    {  // a deferred overflow of an earlier call on this device is reported now
-        int device = 0;
-        if (hipGetDevice(&device) == hipSuccess && take_status(device) != KMC_OK) return KMC_ERR_CAPACITY;
-    }
     int64_t bias = 0;
-    const kmc_dense_args al = aligned_args(a0, bias);
+    kmc_dense_args al = aligned_args(a0, bias);
     const kmc_dense_args *a = &al;
+    if (!al.status) {  // the device's flag (kmc_dense_status)
+        int device = 0;
+        hipError_t he = hipGetDevice(&device);
+        if (he != hipSuccess) return (int)he;
+        uint32_t *sh = nullptr, *sd = nullptr;
+        const int e = status_flag(device, &sh, &sd);
+        if (e) return e;
+        al.status = reinterpret_cast<int32_t *>(sd);
+    }
     if (a->k > 8) return radix_dense(a, bias, stream, false, nullptr);
     Request q{};
     q.data = a->data;
@@ -1073,6 +1087,7 @@ extern "C" int kmc_count_dense_ex(const kmc_dense_args *a0, hipStream_t stream) 
     q.rh = (int64_t)a->read_hi;
     q.ws = a->workspace;
     q.ws_bytes = a->workspace_bytes;
+    q.status = reinterpret_cast<uint32_t *>(a->status);
     return dispatch<int64_t>(a->k, q, stream);
 }
 

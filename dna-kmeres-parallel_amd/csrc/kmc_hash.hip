@@ -998,8 +998,9 @@ struct SortCfg {
     static_assert(CAP <= (uint32_t)(BLOCK * RES) && CAP < 32768u, "K4s sizes");
     static_assert(kSlots == BLOCK * 8, "K4s scan: 8 slot words per thread");
 };
+constexpr uint32_t kSortCapBigCfg = 12288;  // the big instance's cap (sort_list tells the instances apart by it)
 using SortSmall = SortCfg<512, 12, 6080, 12>;   // LDS: 2 workgroups per CU
-using SortBig = SortCfg<1024, 12, 12288, 13>;   // LDS: 1 workgroup per CU
+using SortBig = SortCfg<1024, 12, kSortCapBigCfg, 13>;   // LDS: 1 workgroup per CU
 constexpr int kSortBlock = SortSmall::kBlock;
 constexpr uint32_t kSortCap = SortSmall::kCap;
 constexpr uint32_t kSortCapBig = SortBig::kCap;
@@ -1102,7 +1103,11 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         // does not count only makes its own vmcnt waits stricter (completion is in
         // order), and the next list's vmcnt(0) above retires it; the last list
         // prefetches nothing, so none is in flight when the workgroup ends.
-        const uint64_t nn = ne0 - nb0 <= (uint64_t)C::kCap ? ne0 - nb0 : 0;  // (longer: another kernel's)
+        // (a list this instance will not take -- longer than its cap, which the test
+        // hooks may lower below kCap -- is another kernel's: not prefetched, so no
+        // DMA into this workgroup's LDS is left in flight by a list it skips)
+        const uint64_t lim = C::kCap == kSortCapBigCfg ? p.sort_cap_big : p.sort_cap;
+        const uint64_t nn = ne0 - nb0 <= (lim < (uint64_t)C::kCap ? lim : (uint64_t)C::kCap) ? ne0 - nb0 : 0;
         if ((uint64_t)tid * 16u < nn) {
             const uint64_t a = (uint64_t)(p.ent + nb0 + (uint64_t)tid * 16u);
             asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(a), "s"(lds_off(&S.pfs[0]))
@@ -1595,6 +1600,9 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     char *ws;
     if (workspace) {
         if (workspace_bytes < total) return KMC_ERR_WORKSPACE;
+        // the layout's offsets are 256-byte multiples, and K3b / K4s move whole
+        // 16-byte pieces (and LDS-DMA dwords) of it
+        if (reinterpret_cast<uintptr_t>(workspace) & 255u) return KMC_ERR_ALIGNMENT;
         ws = static_cast<char *>(workspace);
     } else {
         std::lock_guard<std::mutex> lk(h_mu);

@@ -315,6 +315,11 @@ int run(const Options &o) {
     }
     HIPCHK(hipEventRecord(ev[3], st));
     HIPCHK(hipEventSynchronize(ev[3]));
+    if (o.gpus <= 1) {  // the deferred status of the (asynchronous) count on this device
+        int dev = 0;
+        HIPCHK(hipGetDevice(&dev));
+        KMCCHK(kmc_dense_status(dev));
+    }
     const float t1 = ms_between(ev[2], ev[3]);
     if (!o.quiet) {
         printf("Elapsed parallel timer step 1: %g ms, %g secs\n", t1, t1 / 1000);  // main.cu:300

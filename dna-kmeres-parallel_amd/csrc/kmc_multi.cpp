@@ -74,6 +74,8 @@ struct DevState {
     size_t inv_cap = 0;
     void *ws = nullptr;
     size_t ws_cap = 0;
+    int32_t *status = nullptr;  // this call's dense status word on the device (kmc_dense_args::status)
+    size_t status_cap = 0;
     int rc = KMC_OK;  // result of this call's load + count (written by its worker thread)
 };
 
@@ -99,6 +101,7 @@ void free_state(DevState &d) {  // caller holds d.mu
     (void)hipFree(d.sum);
     (void)hipFree(d.inv);
     (void)hipFree(d.ws);
+    (void)hipFree(d.status);
     for (int j = 0; j < 2; ++j) {
         if (d.pin[j]) (void)hipHostFree(d.pin[j]);
         if (d.done[j]) (void)hipEventDestroy(d.done[j]);
@@ -112,7 +115,8 @@ void free_state(DevState &d) {  // caller holds d.mu
     d.sum = nullptr;
     d.inv = nullptr;
     d.ws = nullptr;
-    d.data_cap = d.idx_cap = d.sum_cap = d.inv_cap = d.ws_cap = 0;
+    d.status = nullptr;
+    d.data_cap = d.idx_cap = d.sum_cap = d.inv_cap = d.ws_cap = d.status_cap = 0;
 }
 
 // Grow a cached device buffer to at least `bytes` (contents are not kept).
@@ -182,6 +186,7 @@ void load_and_count(DevState &d, const char *data, const int64_t *indices, uint6
     if (!reserve(d.idx, d.idx_cap, (num_seqs + 1) * sizeof(int64_t))) return bad(KMC_ERR_NOMEM);
     if (!reserve(d.sum, d.sum_cap, sum_bytes)) return bad(KMC_ERR_NOMEM);
     if (want_invalid && !reserve(d.inv, d.inv_cap, num_seqs * sizeof(int32_t))) return bad(KMC_ERR_NOMEM);
+    if (!reserve(d.status, d.status_cap, sizeof(int32_t))) return bad(KMC_ERR_NOMEM);
     kmc_dense_args a{};
     a.data = d.data - base;
     a.indices = d.idx;
@@ -194,13 +199,15 @@ void load_and_count(DevState &d, const char *data, const int64_t *indices, uint6
     a.read_hi = sh.read_hi;
     a.win_lo = sh.win_lo;
     a.win_hi = sh.win_hi;
+    a.status = d.status;  // this shard's own status: another caller's failure is never reported here
     const size_t wsb = kmc_count_dense_ex_workspace_size(&a, d.dev);
     if (wsb == 0 || !reserve(d.ws, d.ws_cap, wsb)) return bad(KMC_ERR_NOMEM);
     a.workspace = d.ws;
     a.workspace_bytes = d.ws_cap;
     // indices are small: one copy, ordered before the count on the same stream
     if (hipMemcpyAsync(d.idx, indices, (num_seqs + 1) * sizeof(int64_t), hipMemcpyHostToDevice, d.st) !=
-        hipSuccess)
+            hipSuccess ||
+        hipMemsetAsync(d.status, 0, sizeof(int32_t), d.st) != hipSuccess)
         return bad(KMC_ERR_NOMEM);
     uint64_t done = 0;
     for (int j = 0; done < len; j ^= 1) {
@@ -259,6 +266,13 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     }
     for (auto *d : b)
         if (d->rc) {
+            // the other devices' copies and counts may still run: let them finish
+            // before the call returns (their buffers stay cached for the next call)
+            for (auto *o : b)
+                if (o->st) {
+                    (void)hipSetDevice(o->dev);
+                    (void)hipStreamSynchronize(o->st);
+                }
             (void)hipSetDevice(cur);
             return d->rc;
         }
@@ -285,6 +299,14 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
         }
         if (!comm_ok) nr = ncclSystemError;
     }
+    int st = KMC_OK;  // every device has synchronised: the shards' own status words
+    if (nr == ncclSuccess)
+        for (auto *d : b) {
+            int32_t v = 0;
+            (void)hipSetDevice(d->dev);
+            if (hipMemcpy(&v, d->status, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) nr = ncclSystemError;
+            else if (v != KMC_OK && st == KMC_OK) st = v;
+        }
     if (nr == ncclSuccess) {
         DevState &d = *b[0];
         (void)hipSetDevice(d.dev);
@@ -297,9 +319,6 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     if (!comm_ok) drop_comms(devs);
     (void)hipSetDevice(cur);
     if (nr != ncclSuccess) return KMC_ERR_RCCL;
-    int st = KMC_OK;  // every device has synchronised: a deferred count overflow is reported now
-    for (auto *d : b)
-        if (kmc_dense_status(d->dev) != KMC_OK) st = KMC_ERR_CAPACITY;
     return st;
 }
 

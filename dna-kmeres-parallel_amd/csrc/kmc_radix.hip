@@ -118,6 +118,7 @@ struct RParams {
     uint32_t *ovf_cnt;   // [G]
     uint32_t ovf_cap;
     float cap_scale;     // test hook: capacities scaled (< 1 forces overflows)
+    uint32_t *status;    // the call's status word (kmc_dense_args::status, set by kmc_count_dense_ex)
 };
 
 // A launch of the exact rerun returns at once unless the sampled pass overflowed.
@@ -847,6 +848,14 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
     bool dirty = true;  // (KMC_R4_FUSE: the list-end pass leaves the bins cleared)
     for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
         const int64_t s = list / p.nbk, b = list % p.nbk;
+        if (b == 0 && threadIdx.x == 0 && p.status) {  // int32 bins of >= 2^31 windows could wrap
+            const Geom g = make_geom<int64_t>(p);
+            int64_t ca, ce;
+            record_windows<K, int64_t>(p, g, s, ca, ce);
+            if (ce - ca >= ((int64_t)1 << 31))
+                __hip_atomic_store(p.status, (uint32_t)KMC_ERR_RECORD_TOO_LONG, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (!KMC_R4_FUSE || dirty)
             for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         if (threadIdx.x == 0) s_sum = 0ull;
@@ -1164,6 +1173,7 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
     p.ovf_cap = 0;
     p.ent_cap = (uint64_t)ent_cap;
     p.cap_scale = cap_scale;
+    p.status = reinterpret_cast<uint32_t *>(a->status);
     uint64_t *bsum = reinterpret_cast<uint64_t *>(base + L.bsum);
     const int64_t nbins = (int64_t)1 << (2 * K);
     const unsigned hist_grid = (unsigned)std::min<int64_t>(n * p.nbk, kMaxGridX);

@@ -31,6 +31,7 @@ DIALECT_NONL = 1   # importSeqsNoNL
 MAX_SEQS_REFERENCE = 100
 DROPIN_K = 3
 KMC_ERR_CAPACITY = 1009
+KMC_ERR_RECORD_TOO_LONG = 1010
 
 
 class KmcError(RuntimeError):
@@ -49,7 +50,7 @@ class DenseArgs(ctypes.Structure):
         ("data", _P), ("indices", _P), ("num_seqs", _U64), ("k", ctypes.c_int),
         ("sum", _P), ("sum_ld", _U64), ("invalid", _P),
         ("read_lo", _U64), ("read_hi", _U64), ("win_lo", _U64), ("win_hi", _U64),
-        ("workspace", _P), ("workspace_bytes", ctypes.c_size_t),
+        ("workspace", _P), ("workspace_bytes", ctypes.c_size_t), ("status", _P),
     ]
 
 
@@ -98,10 +99,31 @@ class diag:
         return False
 
 
+def hip_runtimes():
+    """Paths of the HIP runtime libraries (libamdhip64) mapped into this process."""
+    with open("/proc/self/maps") as f:
+        return sorted(set(line.split()[-1] for line in f if "/libamdhip64.so" in line))
+
+
 def _load(path):
+    """One HIP runtime per process: torch ships its own libamdhip64 (torch/lib),
+    libkmc.so names the SONAME libamdhip64.so.7 (found through its RUNPATH in
+    /opt/rocm/lib).  The dynamic loader satisfies a NEEDED entry with an already
+    loaded library of that SONAME, so torch is imported FIRST (when it is
+    installed) and libkmc then binds to torch's runtime; loaded the other way
+    round, both runtimes would be mapped and each would initialise the GPU on its
+    own.  A second runtime mapped anyway is refused here."""
     if not os.path.exists(path):
         raise RuntimeError("%s not built: run `make -C %s` (no CPU fallback exists)" % (os.path.basename(path), HERE))
+    try:
+        import torch  # noqa: F401  (maps torch's HIP runtime before libkmc's NEEDED entry is resolved)
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
+    rt = hip_runtimes()
+    if len(rt) > 1:
+        raise RuntimeError("two HIP runtimes are mapped in this process (%s): load %s after importing torch, "
+                           "not before" % (", ".join(rt), os.path.basename(path)))
     L.kmc_error_string.restype = ctypes.c_char_p
     L.kmc_error_string.argtypes = [ctypes.c_int]
     L.kmc_version.restype = ctypes.c_int
@@ -216,9 +238,11 @@ def count_dense(data, indices, k, data_bytes=None, invalid=False, workspace=None
 
 
 def dense_args(data, indices, k, out, read=(0, None), win=(0, None), ld=0, invalid=None, workspace=None,
-               data_offset=0):
+               data_offset=0, status=None):
     """Build a kmc_dense_args.  `data_offset` = global offset of data[0] (the data
-    pointer handed to the library is data_ptr - data_offset)."""
+    pointer handed to the library is data_ptr - data_offset).  `status`: an int32
+    device tensor (zeroed by the caller) that receives this call's deferred status
+    (see dense_status_check); None: the device's flag (kmc_dense_status)."""
     a = DenseArgs()
     a.data = ctypes.c_void_p(data.data_ptr() - data_offset)
     a.indices = ctypes.c_void_p(indices.data_ptr())
@@ -234,7 +258,21 @@ def dense_args(data, indices, k, out, read=(0, None), win=(0, None), ld=0, inval
     if workspace is not None:
         a.workspace = ctypes.c_void_p(workspace.data_ptr())
         a.workspace_bytes = workspace.numel() * workspace.element_size()
+    a.status = _dptr(status)
     return a
+
+
+def dense_status_check(status=None, device=None):
+    """Raise KmcError for a failed asynchronous dense call (synchronises first):
+    `status` = the call's own int32 status tensor, or None for the device's flag
+    (kmc_dense_status, which it clears)."""
+    import torch
+    torch.cuda.synchronize()
+    if status is not None:
+        _check(int(status.reshape(-1)[0].item()), "dense count (deferred status)")
+    else:
+        dv = torch.cuda.current_device() if device is None else device
+        _check(lib().kmc_dense_status(dv), "dense count (kmc_dense_status)")
 
 
 def count_dense_ex(args, stream=None):
@@ -444,7 +482,7 @@ _hip_lib = None
 def _hip():
     global _hip_lib
     if _hip_lib is None:
-        _hip_lib = ctypes.CDLL("libamdhip64.so")
+        _hip_lib = ctypes.CDLL("libamdhip64.so.7")  # by SONAME: the runtime libkmc.so is bound to
         _hip_lib.hipMemcpy.argtypes = [_P, _P, ctypes.c_size_t, ctypes.c_int]
         _hip_lib.hipFree.argtypes = [_P]
     return _hip_lib

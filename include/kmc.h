@@ -58,13 +58,14 @@ enum kmc_status {
     KMC_OK = 0,
     KMC_ERR_INVALID_ARG = 1001,   /* null pointer, bad size, bad range */
     KMC_ERR_UNSUPPORTED_K = 1002, /* k outside the supported range of the entry point */
-    KMC_ERR_ALIGNMENT = 1003,     /* data pointer not 16-byte aligned */
+    KMC_ERR_ALIGNMENT = 1003,     /* pointer not aligned as the entry point requires */
     KMC_ERR_WORKSPACE = 1004,     /* caller workspace smaller than *_workspace_size() */
     KMC_ERR_IO = 1005,            /* file cannot be opened/read */
     KMC_ERR_NOMEM = 1006,         /* host or device allocation failed */
     KMC_ERR_RCCL = 1007,          /* RCCL call failed */
     KMC_ERR_NO_DEVICE = 1008,     /* no HIP device visible */
-    KMC_ERR_CAPACITY = 1009       /* caller output smaller than the result (size reported) */
+    KMC_ERR_CAPACITY = 1009,      /* caller output smaller than the result (size reported) */
+    KMC_ERR_RECORD_TOO_LONG = 1010 /* a record has >= 2^31 windows in one dense call: int32 counts could wrap */
 };
 
 /* Human-readable text for a kmc_status or hipError_t code (static storage). */
@@ -105,7 +106,15 @@ KMC_API int sumKmereCoincidencesGlobalMemory_hip(char *data, int *indices, unsig
  *               every NULL-workspace call on that device: such calls must not
  *               overlap (one stream, or the caller serialises them), and they are
  *               not graph-capture safe.  Concurrent calls pass their own workspace.
- * The same holds for the NULL workspace of kmc_pair_distances.  */
+ * The same holds for the NULL workspace of kmc_pair_distances.
+ * Counts are int32 like the reference's (main.cu:598,637: int counters, and the
+ * kernel's int sum, kernels.h:142), which never meets a record of 2^31 windows
+ * (its loader's int offsets stop at 2 GiB).  The 64-bit offsets here do, so a call
+ * in which some record has 2^31 or more windows in range (valid or not) reports
+ * KMC_ERR_RECORD_TOO_LONG through the call's deferred status (below) rather than
+ * passing bins or invalid counts that may have wrapped as valid: count such a record in
+ * window ranges of fewer than 2^31 windows (kmc_count_dense_ex) and add the parts
+ * in 64-bit integers.  The offsets live on the device, so the check runs there. */
 KMC_API size_t kmc_count_dense_workspace_size(int k, uint64_t num_seqs, uint64_t data_bytes, int device);
 
 KMC_API int kmc_count_dense(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes,
@@ -129,20 +138,29 @@ typedef struct kmc_dense_args {
     uint64_t win_lo, win_hi;
     void *workspace;
     size_t workspace_bytes;
+    int32_t *status;         /* optional device-visible int32 (device memory or host-mapped), zeroed by
+                                the caller before the call: this call's kernels store a kmc_status code
+                                in it (KMC_ERR_CAPACITY, KMC_ERR_RECORD_TOO_LONG) when its counts are
+                                not valid; read it after the stream has synchronised.  NULL: the
+                                device's library flag, reported by kmc_dense_status(). */
 } kmc_dense_args;
 
 KMC_API size_t kmc_count_dense_ex_workspace_size(const kmc_dense_args *args, int device);
 KMC_API int kmc_count_dense_ex(const kmc_dense_args *args, hipStream_t stream);
 
-/* Deferred device-side status of the asynchronous dense calls on `device`.  The
- * k = 8 kernel keeps its 16-bit counters exact with spill entries whose number per
- * workgroup is bounded analytically (one per >= 4096 windows); should a workgroup
- * ever emit more than its workspace holds, the kernel raises a flag in host-mapped
- * memory instead of returning short counts silently.  This call (after the stream
- * has synchronised) returns KMC_ERR_CAPACITY if any call on the device raised it
- * since the last query, KMC_OK otherwise, and clears it; a dense call that finds
- * the flag raised at entry also returns KMC_ERR_CAPACITY (and clears it), as does
- * kmc_count_multi after its synchronisation. */
+/* Deferred device-side status of the asynchronous dense calls on `device` that
+ * passed no status word of their own (kmc_count_dense, the drop-in, and
+ * kmc_count_dense_ex with status == NULL).  Two conditions are detected on the
+ * device, where the offsets live: (1) the k = 8 kernel keeps its 16-bit counters
+ * exact with spill entries whose number per workgroup is bounded analytically (one
+ * per >= 4096 windows); should a workgroup ever emit more than its workspace holds,
+ * the counts would be short: KMC_ERR_CAPACITY; (2) a record with 2^31 or more
+ * windows in range: KMC_ERR_RECORD_TOO_LONG (above).  The kernels store the code in
+ * a host-mapped word of the device.  This call (after the stream has synchronised)
+ * returns the code stored since the last query, KMC_OK if none, and clears it.
+ * No other entry point reads or clears it, so a failure is never reported to an
+ * unrelated later call; callers that run dense calls concurrently on one device
+ * pass each call its own status word instead. */
 KMC_API int kmc_dense_status(int device);
 
 /* ------------------------------------------------------------------------ */
@@ -172,7 +190,13 @@ KMC_API int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, in
  * reused until kmc_multi_release().  Thread-safe: a call holds its devices (locked
  * in ascending order) from load to copy-back, so calls whose sets share a device
  * take turns (RCCL communicators are not reentrant), calls on disjoint sets run
- * concurrently, and a set whose collective failed is rebuilt by the next call. */
+ * concurrently, and a set whose collective failed is rebuilt by the next call.
+ * Each shard's count carries its own status word: KMC_ERR_CAPACITY /
+ * KMC_ERR_RECORD_TOO_LONG (kmc_count_dense_ex) are returned by this call.
+ * Retention: the cached per-device buffers are sized to the largest shard + halo
+ * seen (GBs per device for Gbase inputs) plus 64 MB of pinned staging, and are
+ * held until kmc_multi_release().  kmc_set_reserved_cus does not apply here (the
+ * worker threads count with every CU). */
 KMC_API int kmc_count_multi(const char *data, const int64_t *indices, uint64_t num_seqs, uint64_t data_bytes, int k,
                     int ndev, const int *devices, int32_t *sum, int32_t *invalid);
 /* Destroys the communicators and frees the per-device state cached by
@@ -231,7 +255,9 @@ KMC_API int minKmeres2_hip(int *sums, float *mins, int num_seqs, int current_seq
  * workspace, about 20 bytes per window (no hash table lives in HBM), is
  * library-owned here (one per device, grown on demand, shared by the calls on that
  * device, which must not overlap); kmc_count_canonical_hash_ex takes the caller's
- * instead, of kmc_count_canonical_workspace_size() bytes (NULL: library-owned). */
+ * instead, of kmc_count_canonical_workspace_size() bytes (NULL: library-owned),
+ * 256-byte aligned (KMC_ERR_ALIGNMENT otherwise; hipMalloc's pointers are).  The
+ * size is that of a call on `device` (it depends on the device's CU count). */
 #define KMC_CANON_MAX_K 31
 #define KMC_CANON_SOFTMASK 1u
 #define KMC_CANON_FORWARD 2u

@@ -1,0 +1,40 @@
+# GPU box steps, chained: the one parameterised entry for `gpurun` (replaces the
+# round-by-round one-off scripts, which live on in git history).
+#   usage: bash scripts/gpu_run.sh TAG STEP [STEP ...]
+#   steps: tests[:EXPR]   pytest -m gpu (EXPR: a -k expression)
+#          abi            the CPU ABI tests in a process of their own (no torch first)
+#          smoke          __graft_entry__.smoke()
+#          bench          python bench.py (the driver's default line)
+#          profile        scripts/profile_bench.sh: kernel trace + HBM and LDS PMC passes
+#          cbench[:CFGS]  scripts/cbench.py --configs CFGS (default c1,c3,c4,c4r) under the kernel trace
+#          shard          scripts/shardbench.py (one rank's step of an N-way job, N = 1, 2, 4, 8)
+#          fuzz           the dense and canonical fuzzers
+# Every step has its own time limit; the first failing step ends the call.
+# Output: gpurun_out/TAG/<step>.log (+ rocprofv3 directories).
+cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp
+TAG=$1; shift
+O=gpurun_out/$TAG && mkdir -p $O
+run() {  # run LIMIT LOG CMD...: stop the whole call on failure
+    local lim=$1 log=$2; shift 2
+    timeout -k 10 $lim "$@" > $log 2>&1; local rc=$?
+    echo "[$(basename $log .log)] rc=$rc"; tail -3 $log
+    if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED|Killed" $log | head -20; exit $rc; fi
+}
+PYT="python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread"
+for s in "$@"; do
+    case $s in
+        tests) run 1100 $O/tests.log $PYT tests -m gpu --durations=15 ;;
+        tests:*) run 900 $O/tests.log $PYT tests -m gpu -k "${s#tests:}" ;;
+        abi) run 300 $O/abi.log $PYT tests/test_abi.py ;;
+        smoke) run 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run 600 $O/bench.log python bench.py; grep '^{' $O/bench.log > $O/bench.json ;;
+        profile) run 1100 $O/profile.log bash scripts/profile_bench.sh ;;
+        cbench) run 900 $O/cbench.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/cbench_prof -o cb \
+                    -- python3 scripts/cbench.py --iters 3 ;;
+        cbench:*) run 900 $O/cbench.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/cbench_prof -o cb \
+                      -- python3 scripts/cbench.py --iters 3 --configs "${s#cbench:}" ;;
+        shard) run 600 $O/shard.log python scripts/shardbench.py ;;
+        fuzz) run 600 $O/fuzz_dense.log python scripts/fuzz_dense.py && run 600 $O/fuzz_canonical.log python scripts/fuzz_canonical.py ;;
+        *) echo "unknown step $s"; exit 2 ;;
+    esac
+done

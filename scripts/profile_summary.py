@@ -4,6 +4,8 @@
   profiles/<tag>_bench_trace.json   the bench JSON line printed under the profiler
   profiles/<tag>_kernel_launches.json  per-launch durations of the histogram kernel
   profiles/pmc_dense_k8_10gbase.json  HBM bytes per histogram launch (bench.py reads it)
+  profiles/pmc_lds_k8_10gbase.json   LDS-array cycles per window and the held clock of the
+                                     histogram kernel (bench.py's roofline.lds_floor_*)
 FETCH_SIZE is counted in KiB and, on gfx950, reads half the bytes of a wide
 streaming read (MI355X_MICROARCH.md §HBM): bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024."""
 import csv
@@ -18,14 +20,52 @@ SRC = os.path.join(REPO, "gpurun_out", "prof_bench")
 DST = os.path.join(REPO, "profiles")
 
 
-def per_launch(counter_dir, counter, name_sub):
-    vals = []
+def per_launch(counter_dir, counter, name_sub, durations=False):
+    vals, durs = [], []
     for f in glob.glob(os.path.join(counter_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row["Counter_Name"] == counter and name_sub in row["Kernel_Name"]:
                     vals.append(float(row["Counter_Value"]))
-    return vals
+                    durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
+    return (vals, durs) if durations else vals
+
+
+def lds_summary(line, k, kern, cus=256, xcds=8, last=10):
+    """profiles/pmc_lds_k8_10gbase.json from the LDS pass: per full-size launch (the
+    last `last`, after the clock ramp) the LDS-array cycles (all CUs), conflict
+    cycles, LDS atomics, and the kernel's shader cycles (GRBM_GUI_ACTIVE / 8 XCDs)."""
+    d = os.path.join(SRC, "lds")
+    act = per_launch(d, "SQ_LDS_IDX_ACTIVE", kern)
+    con = per_launch(d, "SQ_LDS_BANK_CONFLICT", kern)
+    atm = per_launch(d, "SQ_INSTS_LDS_ATOMIC", kern)
+    grbm, dur = per_launch(d, "GRBM_GUI_ACTIVE", kern, durations=True)
+    if not (act and con and atm and grbm and line):
+        return None
+    full = lambda xs: [i for i, v in enumerate(xs) if v > 0.5 * max(xs)][-last:]  # not the slice check
+    mean = lambda xs, ix: sum(xs[i] for i in ix) / len(ix)
+    ka, kg = full(act), full(grbm)
+    windows = line["config"]["total_records"] * (line["config"]["record_len"] - k + 1)
+    a, c, t = mean(act, ka), mean(con, ka), mean(atm, ka)
+    cyc = mean(grbm, kg) / xcds  # shader cycles of one launch
+    ms = mean(dur, kg)
+    out = {
+        "k": k, "kernel": kern, "windows_per_launch": windows, "cus": cus, "launches": len(ka),
+        "sq_lds_idx_active": a, "sq_lds_bank_conflict": c, "sq_insts_lds_atomic": t,
+        "array_cycles_per_atomic": a / t, "conflict_frac": c / a,
+        "array_cycles_per_window": a / windows,  # summed over the CUs
+        "kernel_cycles": cyc, "launch_ms_under_pmc": ms, "clock_ghz": cyc / (ms * 1e-3) / 1e9,
+        # the binding roof: the share of the kernel's cycles in which an average CU's
+        # LDS array is busy (1.0 = the kernel runs at the LDS floor)
+        "lds_busy_frac": a / cus / cyc,
+        "source": "rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS_ATOMIC GRBM_GUI_ACTIVE of "
+                  "python3 bench.py --steps 20 --warmup 14 (scripts/profile_bench.sh), the last %d full-size "
+                  "launches; kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs (MI355X_MICROARCH.md DVFS note); "
+                  "lds_busy_frac = SQ_LDS_IDX_ACTIVE / CUs / kernel cycles" % len(ka),
+    }
+    with open(os.path.join(DST, "pmc_lds_k8_10gbase.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    return out
 
 
 def main():
@@ -83,6 +123,9 @@ def main():
         with open(os.path.join(DST, "pmc_dense_k8_10gbase.json"), "w") as fh:
             json.dump(out, fh, indent=1)
         print(json.dumps(out))
+    lds = lds_summary(line, k, kern)
+    if lds:
+        print(json.dumps(lds))
 
 
 if __name__ == "__main__":

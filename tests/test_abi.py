@@ -89,3 +89,26 @@ def test_synth_indices_and_host_generator(kmc):
     b = kmc.synth_host(2, 10, seed=0x5EED0008)
     c = kmc.synth_host(1, 10, seed=0x5EED0008, first_base=10)
     np.testing.assert_array_equal(b[11:22], c)
+
+
+def _runtimes_in_child(code):
+    import json
+    import os
+    import sys
+    pkg = os.path.dirname(os.path.abspath(__import__("kmc").__file__))
+    prog = "import sys, json; sys.path.insert(0, %r)\n%s\nimport kmc\nprint(json.dumps(kmc.hip_runtimes()))" % (
+        pkg, code)
+    out = subprocess.run([sys.executable, "-c", prog], check=True, capture_output=True, text=True, timeout=300)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_one_hip_runtime_per_process():
+    """kmc._load imports torch before libkmc.so, so the library binds to the HIP
+    runtime torch ships (the SONAME libamdhip64.so.7 is already loaded) instead of
+    mapping /opt/rocm's beside it -- whichever of kmc and torch the caller touches
+    first.  Checked in fresh processes through /proc/self/maps (no device needed)."""
+    for code in ("import kmc; kmc.lib()\nimport torch",
+                 "import torch\nimport kmc; kmc.lib()",
+                 "import kmc; kmc.lib(); kmc._hip()\nimport torch"):
+        rt = _runtimes_in_child(code)
+        assert len(rt) == 1, (code, rt)

@@ -557,10 +557,13 @@ def test_count_multi_single_device(kmc, oracle, cuda):
 def test_dense_spill_overflow_raises_status(kmc, oracle, cuda):
     """k = 8 spill lists past their capacity are never silent: with the capacity
     lowered to 1 entry (diagnostic library) a 64 MB poly-A record (every workgroup's
-    piece wraps its AAAAAAAA counter ~4 times: several wrap entries each) raises the
-    host-mapped flag, which kmc_dense_status reports once and clears, and which the
-    next dense call reports at entry; with the capacity restored the counts are the
-    oracle's and nothing is raised."""
+    piece wraps its AAAAAAAA counter ~4 times: several wrap entries each) stores
+    KMC_ERR_CAPACITY in the call's status.  Without a status word of its own that is
+    the device's host-mapped flag, which kmc_dense_status reports once and clears,
+    and which no other call consumes (the next unrelated call used
+    to fail in its place); with its own status word (kmc_dense_args::status) the
+    call's failure stays in that word and the device flag is untouched.  With the
+    capacity restored the counts are the oracle's and nothing is raised."""
     import torch
     rng = np.random.default_rng(404)
     acgt = np.frombuffer(b"ACGT", np.uint8)
@@ -571,25 +574,82 @@ def test_dense_spill_overflow_raises_status(kmc, oracle, cuda):
     exp, exp_inv = oracle.count_dense(data, idx, 8)
     d, di = dev(data, cuda), dev(idx, cuda)
     dv = torch.cuda.current_device()
+    small, sidx = random_records(rng, [5000, 70_000])
+    ds, dsi = dev(small, cuda), dev(sidx, cuda)
     with kmc.diag() as D:
         assert D.kmc_dense_status(dv) == 0
         assert D.kmc_diag_dense_spill_cap(1) == 0
         kmc.count_dense(d, di, 8, data_bytes=data.size)
         torch.cuda.synchronize()
-        assert D.kmc_dense_status(dv) == 1009
+        assert D.kmc_dense_status(dv) == kmc.KMC_ERR_CAPACITY
         assert D.kmc_dense_status(dv) == 0  # reported once
         kmc.count_dense(d, di, 8, data_bytes=data.size)
+        out_s, _ = kmc.count_dense(ds, dsi, 8, data_bytes=small.size)  # an unrelated call: not failed by it
         torch.cuda.synchronize()
-        with pytest.raises(kmc.KmcError) as e:  # the next call reports it at entry
-            kmc.count_dense(d, di, 8, data_bytes=data.size)
-        assert e.value.code == 1009
+        assert D.kmc_dense_status(dv) == kmc.KMC_ERR_CAPACITY
+        np.testing.assert_array_equal(out_s.cpu().numpy(), oracle.count_dense(small, sidx, 8)[0])
+        # the call's own status word
+        st = torch.zeros(1, dtype=torch.int32, device=cuda)
+        out = torch.empty((1 << 16, idx.size - 1), dtype=torch.int32, device=cuda)
+        kmc.count_dense_ex(kmc.dense_args(d, di, 8, out.view(-1), status=st))
+        with pytest.raises(kmc.KmcError) as e:
+            kmc.dense_status_check(st)
+        assert e.value.code == kmc.KMC_ERR_CAPACITY and D.kmc_dense_status(dv) == 0
         assert D.kmc_diag_dense_spill_cap(0) == 0
+        st.zero_()
+        kmc.count_dense_ex(kmc.dense_args(d, di, 8, out.view(-1), status=st))
+        kmc.dense_status_check(st)
+        np.testing.assert_array_equal(out.cpu().numpy(), exp)
         out, inv = kmc.count_dense(d, di, 8, data_bytes=data.size, invalid=True)
         torch.cuda.synchronize()
         assert D.kmc_dense_status(dv) == 0
     np.testing.assert_array_equal(out.cpu().numpy(), exp)
     np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv)
-    assert kmc.lib().kmc_dense_status(dv) == 0
+
+
+@pytest.mark.parametrize("k", [4, 8, 13])
+def test_dense_record_of_2p31_windows_reports_error(kmc, cuda, k):
+    """int32 counts (the reference's, main.cu:598,637) could wrap for a record of
+    2^31 or more windows, which the 64-bit offsets admit: such a call stores
+    KMC_ERR_RECORD_TOO_LONG in its status (the device flag, or the call's own word);
+    2^31 - 1 windows pass, and the long record counted as two window ranges of the
+    same buffer (kmc_count_dense_ex) is exact: the bins sum to its windows in int64.
+    A 2.15 GB record: k = 4 and 8 on the LDS path, 13 on the radix path."""
+    import torch
+    dv = torch.cuda.current_device()
+    L = (1 << 31) + k  # windows = L - k + 1 = 2^31 + 1
+    buf = torch.empty(L + 1 + 16, dtype=torch.uint8, device=cuda)
+    kmc.synth_fill(buf, 1, L, 0x5EED2031 + k)
+    nb = 1 << (2 * k)
+    out = torch.empty((nb, 1), dtype=torch.int32, device=cuda)
+    for n_win, ok in ((L - k + 1, False), ((1 << 31) - 1, True)):
+        Lr = n_win + k - 1
+        di = dev(np.array([0, Lr + 1], np.int64), cuda)
+        saved = buf[Lr].clone()
+        buf[Lr] = 0  # the record's terminator
+        assert kmc.lib().kmc_dense_status(dv) == 0
+        kmc.count_dense(buf, di, k, data_bytes=Lr + 1, out=out)
+        torch.cuda.synchronize()
+        assert kmc.lib().kmc_dense_status(dv) == (0 if ok else kmc.KMC_ERR_RECORD_TOO_LONG), (k, n_win)
+        st = torch.zeros(1, dtype=torch.int32, device=cuda)
+        kmc.count_dense_ex(kmc.dense_args(buf[:Lr + 1], di, k, out.view(-1), status=st))
+        torch.cuda.synchronize()
+        assert int(st.item()) == (0 if ok else kmc.KMC_ERR_RECORD_TOO_LONG)
+        if not ok:  # two window ranges of < 2^31 windows each, added in int64
+            acc = torch.zeros(nb, dtype=torch.int64, device=cuda)
+            cut = 1 << 30
+            for lo, hi in ((0, cut), (cut, Lr + 1)):
+                st.zero_()
+                kmc.count_dense_ex(kmc.dense_args(buf[:Lr + 1], di, k, out.view(-1), read=(lo, min(hi + k - 1, Lr + 1)),
+                                                  win=(lo, hi), status=st))
+                kmc.dense_status_check(st)
+                acc += out[:, 0].to(torch.int64)
+            assert int(acc.sum()) == n_win
+        else:
+            assert int(out.to(torch.int64).sum()) == n_win
+        buf[Lr] = saved
+    del buf
+    torch.cuda.empty_cache()
 
 
 def test_synth_fill_range_matches_host(kmc, cuda):
