@@ -40,20 +40,10 @@
 #include "kmc_internal.h"
 #include "kmc_stream.h"
 
-// k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
-// spill entries (0: no scans)
-// Round 4: the workgroup's first record found by one load per thread (n <= BLOCK)
-// instead of a binary search by one thread, the LDS histogram cleared and the
-// slab flush done 16 bytes per lane (the fixed part of a launch, which an 8-way
-// shard's step pays on 1/8 of the work)
-#ifndef KMC_DENSE_VEC
-#define KMC_DENSE_VEC 1
-#endif
-#ifndef KMC_HM3_SCAN
-#define KMC_HM3_SCAN 256
-#endif
-
 namespace kmc {
+// k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
+// spill entries (section 4.1 of DESIGN.md: 64 / 256 / 512 / 1 024 measured)
+constexpr int kHm3Scan = 256;
 thread_local hipEvent_t t_trace_before = nullptr;
 thread_local hipEvent_t t_trace_after = nullptr;
 namespace {
@@ -259,12 +249,12 @@ struct DenseOp {
         if constexpr (HM == 3) nwin += MASKED ? (uint32_t)__builtin_popcount(W) : 16u;
     }
     __device__ __forceinline__ void after_iter(int64_t i, int64_t per, bool) {
-        if constexpr (HM == 3 && KMC_HM3_SCAN > 0) {
-            // hot halves (>= 32768) go to spill entries every KMC_HM3_SCAN tiles per
+        if constexpr (HM == 3) {
+            // hot halves (>= 32768) go to spill entries every kHm3Scan tiles per
             // wave, so a half wraps only if one k-mer takes >= 32768 of the
-            // workgroup's NWAVES * KMC_HM3_SCAN * 1024 windows in between (long
+            // workgroup's NWAVES * kHm3Scan * 1024 windows in between (long
             // low-complexity runs); wraps stay detected by the piece total
-            if ((i % KMC_HM3_SCAN) == KMC_HM3_SCAN - 1 && i + 1 < per) {
+            if ((i % kHm3Scan) == kHm3Scan - 1 && i + 1 < per) {
                 lds_barrier();
                 p16_scan<BLOCK, 32768u>(pc);
                 lds_barrier();
@@ -325,7 +315,10 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
         const int64_t R0 = (tb << kTileShift) > g.wl ? (tb << kTileShift) : g.wl;
         const int64_t R1 = (te << kTileShift) < g.wh ? (te << kTileShift) : g.wh;
         int64_t s0 = 0;
-        if (KMC_DENSE_VEC && p.n <= BLOCK) {
+        // (round 4: the first record found by one load per thread when n <= BLOCK,
+        // the LDS cleared and the slab flushed 16 bytes per lane: the fixed part of a
+        // launch, which an 8-way shard's step pays on 1/8 of the work)
+        if (p.n <= BLOCK) {
             // last record s with indices[s] <= R0 (records before it end before R0;
             // the offsets are sorted): the number of such records, less one
             if (tid == 0) {
@@ -356,7 +349,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 misc[1] = (uint32_t)lo;
                 misc[2] = (uint32_t)((uint64_t)lo >> 32);
             }
-            for (int i = tid; i < NW; i += BLOCK) h[i] = 0u;
+            for (int i = tid; i < NW / 4; i += BLOCK) reinterpret_cast<uint4 *>(h)[i] = make_uint4(0u, 0u, 0u, 0u);
             __syncthreads();
             s0 = (int64_t)((uint64_t)misc[1] | ((uint64_t)misc[2] << 32));
         }
@@ -403,7 +396,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 // LDS: the halves are exact, wraps live in spills); the LDS cleared
                 const auto flush = [&]() {
                     uint32_t dsum = 0u;
-                    if (KMC_DENSE_VEC && !entire) {  // the slab: 16 bytes per lane
+                    if (!entire) {  // the slab: 16 bytes per lane
                         for (int i = tid; i < NW / 4; i += BLOCK) {
                             const uint4 v = reinterpret_cast<const uint4 *>(h)[i];
                             reinterpret_cast<uint4 *>(h)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -643,19 +636,10 @@ template <> struct Cfg<1> { static constexpr int R = 32, BLOCK = 512, HM = 0; st
 template <> struct Cfg<2> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<3> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<4> { static constexpr int R = 32, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
-#ifndef KMC_R5
-#define KMC_R5 8
-#endif
-#ifndef KMC_R6
-#define KMC_R6 2
-#endif
-template <> struct Cfg<5> { static constexpr int R = KMC_R5, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
-template <> struct Cfg<6> { static constexpr int R = KMC_R6, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<5> { static constexpr int R = 8, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
+template <> struct Cfg<6> { static constexpr int R = 2, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
 template <> struct Cfg<7> { static constexpr int R = 1, BLOCK = 512, HM = 0; static constexpr bool P16 = false; };
-#ifndef KMC_K8_BLOCK
-#define KMC_K8_BLOCK 1024
-#endif
-template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = KMC_K8_BLOCK, HM = 3; static constexpr bool P16 = true; };
+template <> struct Cfg<8> { static constexpr int R = 1, BLOCK = 1024, HM = 3; static constexpr bool P16 = true; };
 
 struct DevInfo {
     int cus = 0;
@@ -776,7 +760,6 @@ inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
 // windows * (1/32768 + 3/65536) = windows * 5/65536 <= windows / 4096 entries.
 constexpr uint32_t kSpillWindowsPerEntry = 4096;
 static_assert(5u * kSpillWindowsPerEntry <= 65536u, "HM 3 scan + HM 1 recount entries exceed the spill cap");
-static_assert(KMC_HM3_SCAN >= 0, "scan interval");
 inline uint32_t spill_cap_for(int64_t tiles_per_wg) {
     const int64_t windows = tiles_per_wg * kTile;
     return (uint32_t)(windows / kSpillWindowsPerEntry + 64);

@@ -140,6 +140,23 @@ struct HParams {
     uint64_t *rec_off;       // [n + 1] output offsets
     uint64_t *out_keys;
     uint32_t *out_counts;
+    // direct output (round 5, section 4.4 of DESIGN.md): the counting kernels write
+    // each list's pairs to their final place in record r's output region, reserved
+    // from the record's cursor, once r's start is known; otherwise to pk, copied by
+    // canon_fallback_kernel at the end
+    int direct;
+    int32_t *lrec;                // [lists] record of each list
+    unsigned long long *rstate;   // [n] bits 0-39: pairs reserved in r; 40-63: lists of r not yet reserved,
+                                  // counted up from 2^24 - lists(r) (0 once every list has reserved)
+    unsigned long long *rbase;    // [n + 1] start of record r's pairs once known (~0 before)
+    uint64_t *fq;                 // [2 lists][4] (pk offset, record, offset in the record, pairs) to copy
+    unsigned long long *nfq;      // their number
+    uint64_t *tq;                 // the queue this canon_table_kernel launch drains (defer or defer2)
+    unsigned long long *ntq;
+    uint64_t *defer2;             // [lists][3] direct mode: the common instance's deferrals (the table
+    unsigned long long *ndefer2;  // kernel's second launch); defer holds the long lists and the big
+                                  // instance's deferrals (its first launch)
+    int64_t l_lo, l_hi;           // direct mode: the lists of this launch of the common instance
 };
 
 // Partition value of a key: K1 / K3a / K3b bucket and list by its top bits.  A
@@ -679,6 +696,7 @@ __global__ void canon_list_start_kernel(HParams p) {
         if (p.lbase[m] <= l) a = m; else b = m - 1;
     }
     p.list_start[l] = p.off[p.cbase[a] + (l - p.lbase[a]) * p.nwg[a]];
+    if (p.lrec) p.lrec[l] = (int32_t)a;
 }
 
 // K3b: one workgroup per coarse bucket of a record with several lists per bucket;
@@ -725,6 +743,73 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
         rg.round_end();
     }
     rg.finish();
+}
+
+// ---------------------------------------------------------------------------
+// Direct output (round 5).  Record r's pairs occupy [F_r, F_r + D_r) of the output,
+// F_r = D_0 + ... + D_{r-1}; a list reserves its D_l pairs at an offset of r's
+// cursor (rstate) -- the order within a record is unspecified, so any order of
+// reservations is a valid layout -- and writes them to F_r + offset when F_r is
+// already known (rbase[r] != ~0), else to pk for canon_fallback_kernel.  F_r
+// becomes known when every list of records 0 .. r-1 has reserved: the list whose
+// reservation completes record r extends the chain rbase[r + 1] = rbase[r] + D_r
+// as far as the records after it are complete.  Correctness never depends on the
+// chain (a list that finds F_r unknown takes the pk path, and the final scan sets
+// every F_r); the chain only decides how many pairs avoid the copy.
+constexpr int kPairsBits = 40;
+constexpr unsigned long long kPairsMask = (1ull << kPairsBits) - 1ull;
+constexpr unsigned long long kUnknown = ~0ull;
+
+// The chain's words are read and written with read-modify-write atomics only: a
+// plain agent-scope load can be served from this XCD's L2 (MI355X: one L2 per
+// XCD, not coherent with the others within a kernel), where a line cached before
+// another XCD's update still holds the old word -- with loads, C4's chain stopped
+// at record 2 in one run (scripts/canon_direct_probe.py).  The atomics are
+// performed where every XCD's atomics on the word are ordered.
+__device__ __forceinline__ unsigned long long ld_agent(unsigned long long *a) {
+    return __hip_atomic_fetch_add(a, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0), gfx9 encoding
+
+// From record r, whose start F is known: publish the starts of the records after
+// it while they are complete.  Each store is waited for before the next record's
+// state is read, and a completing list reads rbase[r] only after its own
+// reservation returned, so one of the two sees the other's write (the chain never
+// stops at a record that completed while it was being extended).
+__device__ __forceinline__ void chain_from(const HParams &p, int64_t r, unsigned long long F) {
+    for (; r < p.n; ++r) {
+        const unsigned long long v = ld_agent(&p.rstate[r]);
+        if ((v >> kPairsBits) != 0ull) return;  // record r has lists still to reserve
+        F += v & kPairsMask;
+        (void)__hip_atomic_exchange(&p.rbase[r + 1], F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wait_vm();
+    }
+}
+
+// Reserve `cnt` pairs for one list of record r (one thread): returns the list's
+// offset in the record and sets *F to the record's start, or kUnknown.
+__device__ __forceinline__ unsigned long long reserve_pairs(const HParams &p, int64_t r, uint32_t cnt,
+                                                            unsigned long long *F) {
+    const unsigned long long old = __hip_atomic_fetch_add(&p.rstate[r], (unsigned long long)cnt + (1ull << kPairsBits),
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long f = ld_agent(&p.rbase[r]);  // (issued before the add returned: independent)
+    wait_vm();
+    if ((old >> kPairsBits) == (1ull << (64 - kPairsBits)) - 1ull) {  // the last list of r
+        const unsigned long long fr = ld_agent(&p.rbase[r]);        // (after the add)
+        if (fr != kUnknown) chain_from(p, r, fr);
+    }
+    *F = f;
+    return old & kPairsMask;
+}
+
+// A list's pairs left in pk[src, src + cnt), to be copied to record r's offset c
+__device__ __forceinline__ void queue_copy(const HParams &p, uint64_t src, int64_t r, uint64_t c, uint64_t cnt) {
+    if (cnt == 0) return;
+    const unsigned long long i = atomicAdd(p.nfq, 1ull);
+    p.fq[4 * i] = src;
+    p.fq[4 * i + 1] = (uint64_t)r;
+    p.fq[4 * i + 2] = c;
+    p.fq[4 * i + 3] = cnt;
 }
 
 // K4: lists counted in an LDS table, workgroups striding over the lists.  Its
@@ -870,8 +955,8 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
     lds_barrier();
     // the lists canon_sort_kernel left: longer than its capacity, or a key repeated
     // more often than its dedup takes
-    const int64_t G = gridDim.x, nl = (int64_t)*p.ndefer;
-    const uint64_t *dl = p.defer;  // (list, begin, end) triples
+    const int64_t G = gridDim.x, nl = (int64_t)*p.ntq;
+    const uint64_t *dl = p.tq;  // (list, begin, end) triples (defer, or in direct mode defer2)
     int64_t i = blockIdx.x;
     if (i >= nl) return;
     // list bounds two lists ahead, keys one list ahead
@@ -957,7 +1042,15 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
             par ^= 1;
             ++q;
         }
-        if (tid == 0) p.ndist[l] = (uint32_t)(out - b0);
+        if (tid == 0) {
+            if (p.direct) {  // the list's pairs stay in pk: reserved in the record, copied at the end
+                unsigned long long F;
+                const int64_t r = p.lrec[l];
+                queue_copy(p, b0, r, reserve_pairs(p, r, (uint32_t)(out - b0), &F), out - b0);
+            } else {
+                p.ndist[l] = (uint32_t)(out - b0);
+            }
+        }
         b0 = b1;
         e0 = e1;
         b1 = b2;
@@ -988,19 +1081,21 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
 // 8 192-slot table, takes the lists of 6 081 .. 12 288 keys that the
 // first hands it (chromosome-sized records: 2^15 lists of ~7.6 K keys), which
 // until round 3 went to the probed table kernel.
-template <int BLOCK, int RES, uint32_t CAP, int SLOTS_LG>
+template <int BLOCK, int RES, uint32_t CAP, int SLOTS_LG, uint32_t SK, uint32_t RC>
 struct SortCfg {
+    static constexpr uint32_t kSk = SK;                 // sk entries: the list's keys, then staged results
+    static constexpr uint32_t kRc = RC;                 // direct output: staged results' counts
     static constexpr int kBlock = BLOCK;
     static constexpr int kRes = RES;                    // keys per thread
     static constexpr uint32_t kCap = CAP;               // <= kBlock * kRes
     static constexpr int kSlotsLg = SLOTS_LG;
     static constexpr int kSlots = 1 << SLOTS_LG;        // one 32-bit word per slot
-    static_assert(CAP <= (uint32_t)(BLOCK * RES) && CAP < 32768u, "K4s sizes");
+    static_assert(CAP <= (uint32_t)(BLOCK * RES) && CAP < 32768u && CAP <= SK, "K4s sizes");
     static_assert(kSlots == BLOCK * 8, "K4s scan: 8 slot words per thread");
 };
 constexpr uint32_t kSortCapBigCfg = 12288;  // the big instance's cap (sort_list tells the instances apart by it)
-using SortSmall = SortCfg<512, 12, 6080, 12>;   // LDS: 2 workgroups per CU
-using SortBig = SortCfg<1024, 12, kSortCapBigCfg, 13>;   // LDS: 1 workgroup per CU
+using SortSmall = SortCfg<512, 12, 6080, 12, 7456, 1024>;   // LDS: 2 workgroups per CU
+using SortBig = SortCfg<1024, 12, kSortCapBigCfg, 13, 15232, 2048>;   // LDS: 1 workgroup per CU
 constexpr int kSortBlock = SortSmall::kBlock;
 constexpr uint32_t kSortCap = SortSmall::kCap;
 constexpr uint32_t kSortCapBig = SortBig::kCap;
@@ -1015,15 +1110,21 @@ constexpr uint32_t kHotMax = 128;                     // crowded slots per list 
 
 template <class C>
 struct K4sLds {
-    unsigned long long sk[C::kCap];   // the keys of the slots that fail the distinctness test, sorted by slot
+    unsigned long long sk[C::kSk];    // the keys of the slots that fail the distinctness test, sorted by slot
+                                      // (direct output: then the distinct slots' keys, then staged results)
     uint32_t sc[C::kSlots];           // slot words: count | sub-hash sum, then start | count | distinct
     uint32_t hot[kHotMax];            // failing slots holding more than kSortMaxM keys (crowded)
     uint32_t wsum[C::kBlock / 64];
     uint32_t pfs[64];                 // scratch target of the next list's L2 prefetch (never read)
-    uint32_t out;                     // distinct keys emitted
+    uint32_t out;                     // distinct keys emitted (direct output: of the distinct slots)
     uint32_t nhot;
+    uint32_t nres;                    // direct output: (key, count) results of the failing slots
+    uint32_t mode;                    // direct output: the results to their final place (1) or to pk (0)
+    unsigned long long gbase;         // direct output: where the list's pairs go
+    uint32_t rc[C::kRc];              // direct output: the staged results' counts (their keys: sk[n, ...))
 };
 static_assert(sizeof(K4sLds<SortBig>) <= 160 * 1024, "big K4s instance: one workgroup per CU");
+static_assert(sizeof(K4sLds<SortSmall>) <= 80 * 1024, "common K4s instance: two workgroups per CU");
 
 // a list left to another kernel: its id and key range, appended to (q, nq)
 __device__ __forceinline__ void queue_list(uint64_t *q, unsigned long long *nq, int64_t l, uint64_t b, uint64_t e) {
@@ -1051,6 +1152,7 @@ __device__ __forceinline__ void emit_pair(const HParams &p, uint64_t o, unsigned
 
 __device__ __forceinline__ uint32_t half16(uint32_t w, uint32_t hi) { return hi ? (w >> 16) : (w & 0xFFFFu); }
 
+
 // A slot word after the scan: the slot's start in sk (bits 0-15), its key count
 // (16-30) and bit 31 set when its keys are known to be distinct (section 4.4).
 constexpr uint32_t kSlotDistinct = 0x80000000u;
@@ -1059,13 +1161,23 @@ __device__ __forceinline__ uint32_t slot_count(uint32_t w) { return (w >> 16) & 
 // One list of n <= C::kCap keys [b0, e0) counted by the counting sort (the
 // workgroup calls it uniformly).  A list with too many crowded slots is deferred
 // to the table kernel.
-template <class C>
+// DIRECT (round 5): the list's pairs are staged in LDS -- the keys of the
+// distinct slots (count 1) in sk after the failing slots' keys, the failing
+// slots' results after those (keys in sk[n, ...), counts in rc, as many as fit:
+// the rest go to pk) -- and reserved in the record once the list's total is
+// known, then written out in one coalesced pass: to their final place when the
+// record's start is known, else to pk, whose pairs canon_fallback_kernel copies
+// at the end.  (Two reservations -- the distinct slots' keys right
+// after the scan, written from registers -- measured C4 38.7 ms against 35.1 ms,
+// scripts/canon_direct_probe.py.)
+template <class C, bool DIRECT>
 __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_t l, uint64_t b0, uint64_t e0,
                                           uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0) {
     constexpr int kRes = C::kRes, kBlk = C::kBlock, kSlots = C::kSlots;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint64_t lt = (1ull << lane) - 1ull;
+    const int64_t rec = DIRECT ? (int64_t)p.lrec[l] : 0;  // (loaded with the keys)
     unsigned long long kh[kRes];
 #pragma unroll
     for (int j = 0; j < kRes; ++j) {
@@ -1117,6 +1229,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     if (tid == 0) {
         S.out = 0u;
         S.nhot = 0u;
+        S.nres = 0u;
     }
     // rank: one returning add per key on its slot's word, 1 + 2^(16 + sub) with sub
     // four more bits of the key's hash: the low half counts the slot's keys (the
@@ -1174,9 +1287,18 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     lds_barrier();  // C2: slot starts
     const uint32_t nhot = S.nhot;
     if (nhot > kHotMax) {  // too many crowded slots: the probed table counts this list (uniform)
-        if (tid == 0) defer_list(p, l, b0, e0);
+        if (tid == 0) {
+            // (direct output: to the table kernel's second launch, after every other
+            // list; its first takes the lists too long for the big instance)
+            if (DIRECT) queue_list(p.defer2, p.ndefer2, l, b0, e0);
+            else defer_list(p, l, b0, e0);
+        }
         return;  // (the next list's barrier A orders the LDS reuse)
     }
+    const uint32_t na = n - nsk;  // keys of the distinct slots (each a pair of count 1)
+    constexpr bool staged = DIRECT;  // (the distinct slots' keys always fit: n <= kCap <= kSk)
+    // results staged in LDS (the rest to pk[b0 + na + o])
+    const uint32_t rcap = DIRECT ? (C::kSk - n < C::kRc ? C::kSk - n : C::kRc) : 0u;
     // scatter: a key of a distinct slot (alone in it, or all its keys on
     // different subs: ~94 % of the keys of distinct 2-4 K-key lists over 4 096
     // slots) is a key of count 1 and leaves at once; the others go to sk
@@ -1193,7 +1315,11 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
             uint32_t wb = 0u;
             if (lane == 0) wb = atomicAdd(&S.out, (uint32_t)__popcll(am));
             wb = __builtin_amdgcn_readlane(wb, 0);  // (a v_readlane, where __shfl is a ds_bpermute)
-            if (alone) emit_pair(p, b0 + wb + (uint32_t)__popcll(am & lt), kh[j], 1u);
+            if (alone) {
+                const uint32_t o = wb + (uint32_t)__popcll(am & lt);
+                if (staged) S.sk[nsk + o] = kh[j];  // (sk[0, nsk): the failing slots' keys)
+                else emit_pair(p, b0 + o, kh[j], 1u);
+            }
         }
     }
     lds_barrier();  // D: the keys of the failing slots sorted by slot
@@ -1226,9 +1352,17 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         }
         const uint64_t m = __ballot(first);
         uint32_t wb = 0u;
-        if (lane == 0 && m) wb = atomicAdd(&S.out, (uint32_t)__popcll(m));
+        if (lane == 0 && m) wb = atomicAdd(DIRECT ? &S.nres : &S.out, (uint32_t)__popcll(m));
         wb = __builtin_amdgcn_readlane(wb, 0);
-        if (first) emit_pair(p, b0 + wb + (uint32_t)__popcll(m & lt), h, cnt);
+        if (first) {
+            const uint32_t o = wb + (uint32_t)__popcll(m & lt);
+            if (DIRECT && o < rcap) {
+                S.sk[n + o] = h;  // (after the distinct slots' keys)
+                S.rc[o] = cnt;
+            } else {
+                emit_pair(p, b0 + (DIRECT ? na : 0u) + o, h, cnt);
+            }
+        }
     }
     if (nhot) lds_barrier();  // (uniform) the loop above has read sk before the crowded slots' marks
     // crowded slots (a key repeated more than kSortMaxM times hashes there), one
@@ -1269,9 +1403,16 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
             if ((nd & 63u) == 0u || last) {  // (uniform) this batch of results out
                 const uint32_t nb = ((nd - 1u) & 63u) + 1u;
                 uint32_t wb = 0u;
-                if (lane == 0) wb = atomicAdd(&S.out, nb);
+                if (lane == 0) wb = atomicAdd(DIRECT ? &S.nres : &S.out, nb);
                 wb = __builtin_amdgcn_readlane(wb, 0);
-                if ((uint32_t)lane < nb) emit_pair(p, b0 + wb + (uint32_t)lane, myk, myc);
+                if ((uint32_t)lane < nb) {
+                    if (DIRECT && wb + (uint32_t)lane < rcap) {
+                        S.sk[n + wb + (uint32_t)lane] = myk;
+                        S.rc[wb + (uint32_t)lane] = myc;
+                    } else {
+                        emit_pair(p, b0 + (DIRECT ? na : 0u) + wb + (uint32_t)lane, myk, myc);
+                    }
+                }
             }
             if (last) break;
             c = nx;
@@ -1279,24 +1420,60 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         }
     }
     lds_barrier();  // E: every key emitted
-    if (tid == 0) p.ndist[l] = S.out;
+    if constexpr (DIRECT) {
+        // the list's pairs -- the na distinct slots' keys, then the results, of
+        // which those past rcap are in pk[b0 + na + rcap, ...) -- reserved in the
+        // record with the list's completion, then the staged ones written out
+        const uint32_t nres = S.nres, D = na + nres, Ds = na + (nres < rcap ? nres : rcap);
+        if (tid == 0) {
+            unsigned long long F;
+            const unsigned long long c = reserve_pairs(p, rec, D, &F);
+            const bool fin = F != kUnknown;
+            S.mode = fin ? 1u : 0u;
+            S.gbase = fin ? F + c : b0;
+            if (!fin) queue_copy(p, b0, rec, c, D);  // the whole list from pk
+            else queue_copy(p, b0 + Ds, rec, c + Ds, D - Ds);  // (the results past rcap, if any)
+        }
+        lds_barrier();
+        {
+            const bool fin = S.mode != 0u;
+            const unsigned long long g = S.gbase;
+            for (uint32_t i = (uint32_t)tid; i < Ds; i += kBlk) {
+                const bool a = i < na;
+                const unsigned long long h = S.sk[a ? nsk + i : n + (i - na)];
+                const uint32_t cnt = a ? 1u : S.rc[i - na];
+                if (fin) {
+                    p.out_keys[g + i] = unmix62(h);
+                    p.out_counts[g + i] = cnt;
+                } else {
+                    emit_pair(p, g + i, h, cnt);
+                }
+            }
+        }
+    } else {
+        if (tid == 0) p.ndist[l] = S.out;
+    }
 }
 
 // K4s, common instance: every list; those longer than sort_cap go to the big
-// instance (up to sort_cap_big keys) or to the table kernel.
+// instance (up to sort_cap_big keys) or to the table kernel (DIRECT: already
+// queued there by canon_classify_kernel, which runs first).
+template <bool DIRECT>
 __global__ __launch_bounds__(SortSmall::kBlock) __attribute__((amdgpu_waves_per_eu(4))) void canon_sort_kernel(
     HParams p) {
     __shared__ __attribute__((aligned(16))) K4sLds<SortSmall> S;
     uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)
-    if ((int64_t)blockIdx.x < p.lists) {
-        b0 = p.list_start[blockIdx.x];
-        e0 = p.list_start[blockIdx.x + 1];
+    // lists [l_lo, l_hi): all of them, or (DIRECT) one group of records per launch
+    const int64_t l_lo = DIRECT ? p.l_lo : 0, l_hi = DIRECT ? p.l_hi : p.lists;
+    if (l_lo + (int64_t)blockIdx.x < l_hi) {
+        b0 = p.list_start[l_lo + blockIdx.x];
+        e0 = p.list_start[l_lo + blockIdx.x + 1];
     }
-    for (int64_t l = blockIdx.x; l < p.lists; l += gridDim.x) {
+    for (int64_t l = l_lo + blockIdx.x; l < l_hi; l += gridDim.x) {
         const uint32_t n = (uint32_t)(e0 - b0 < 0xFFFFFFFFull ? e0 - b0 : 0xFFFFFFFFull);
-        const uint64_t *nxt = l + gridDim.x < p.lists ? p.list_start + l + gridDim.x : nullptr;
+        const uint64_t *nxt = l + gridDim.x < l_hi ? p.list_start + l + gridDim.x : nullptr;
         if (n > p.sort_cap) {  // workgroup-uniform
-            if (threadIdx.x == 0) {
+            if (!DIRECT && threadIdx.x == 0) {
                 if (n <= p.sort_cap_big) queue_list(p.big, p.nbig, l, b0, e0);
                 else defer_list(p, l, b0, e0);
             }
@@ -1309,7 +1486,7 @@ __global__ __launch_bounds__(SortSmall::kBlock) __attribute__((amdgpu_waves_per_
         // (the next list of this workgroup: its bounds loaded and its keys
         // prefetched into L2 during this one)
         uint64_t nb0, ne0;
-        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0);
+        sort_list<SortSmall, DIRECT>(p, S, l, b0, e0, n, nxt, nb0, ne0);
         b0 = nb0;
         e0 = ne0;
     }
@@ -1317,15 +1494,18 @@ __global__ __launch_bounds__(SortSmall::kBlock) __attribute__((amdgpu_waves_per_
 
 // K4s, big instance: the lists the common instance handed over (workgroups beyond
 // their number exit at once).
+template <bool DIRECT>
 __global__ __launch_bounds__(SortBig::kBlock) void canon_sort_big_kernel(HParams p) {
     __shared__ __attribute__((aligned(16))) K4sLds<SortBig> S;
-    const int64_t nl = (int64_t)*p.nbig;
-    for (int64_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    // DIRECT: one group of records per launch, its segment of the (list-ordered) queue
+    const int64_t q_lo = DIRECT ? (int64_t)p.dist_off[p.l_lo] : 0;
+    const int64_t nl = DIRECT ? (int64_t)p.dist_off[p.l_hi] : (int64_t)*p.nbig;
+    for (int64_t i = q_lo + blockIdx.x; i < nl; i += gridDim.x) {
         const uint64_t b0 = p.big[3 * i + 1], e0 = p.big[3 * i + 2];
         const int64_t in = i + gridDim.x;
         uint64_t nb0, ne0;  // (few lists here: the entries are reloaded per list)
-        sort_list<SortBig>(p, S, (int64_t)p.big[3 * i], b0, e0, (uint32_t)(e0 - b0), in < nl ? p.big + 3 * in + 1 : nullptr,
-                           nb0, ne0);
+        sort_list<SortBig, DIRECT>(p, S, (int64_t)p.big[3 * i], b0, e0, (uint32_t)(e0 - b0),
+                                   in < nl ? p.big + 3 * in + 1 : nullptr, nb0, ne0);
     }
 }
 
@@ -1364,6 +1544,89 @@ __global__ void canon_recoff_kernel(HParams p) {
     if (r <= p.n) p.rec_off[r] = p.dist_off[p.lbase[r]];
 }
 
+// Direct output: per-record state -- no pairs reserved, 2^24 - lists(r) in the
+// list field, so that the last list's reservation carries it to 0 -- and the
+// record starts unknown but the first.
+__global__ void canon_direct_setup_kernel(HParams p) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < p.n) p.rstate[r] = ((1ull << (64 - kPairsBits)) - (unsigned long long)(p.lbase[r + 1] - p.lbase[r]))
+                               << kPairsBits;
+    if (r <= p.n) p.rbase[r] = r == 0 ? 0ull : kUnknown;
+    if (r == 0) *p.nfq = 0ull;
+}
+
+// Direct output: the lists the common K4s instance does not take, by length: a
+// flag per list for the big instance (ndist, scanned into dist_off, then compacted
+// in list order by canon_big_queue_kernel: each group of records takes its own
+// segment), the longer ones to the table kernel's first launch.
+__global__ void canon_classify_kernel(HParams p) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= p.lists) return;
+    const uint64_t b = p.list_start[l], e = p.list_start[l + 1];
+    const bool big = e - b > (uint64_t)p.sort_cap && e - b <= (uint64_t)p.sort_cap_big;
+    p.ndist[l] = big ? 1u : 0u;
+    if (e - b > (uint64_t)p.sort_cap && !big) defer_list(p, l, b, e);
+}
+
+__global__ void canon_big_queue_kernel(HParams p) {
+    const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (l == p.lists) *p.nbig = p.dist_off[l];
+    if (l >= p.lists || !p.ndist[l]) return;
+    const uint64_t i = p.dist_off[l];
+    p.big[3 * i] = (uint64_t)l;
+    p.big[3 * i + 1] = p.list_start[l];
+    p.big[3 * i + 2] = p.list_start[l + 1];
+}
+
+// Direct output, after every list: each record's start (exclusive scan of the
+// records' pair counts: the same values the chain published) -> rbase, rec_off.
+// One workgroup of 1 024 threads, 1 024 records per step.
+__global__ __launch_bounds__(1024) void canon_direct_final_kernel(HParams p) {
+    __shared__ unsigned long long ws[16];
+    __shared__ unsigned long long carry;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) carry = 0ull;
+    __syncthreads();
+    for (int64_t r0 = 0; r0 <= p.n; r0 += 1024) {
+        const int64_t r = r0 + tid;
+        const unsigned long long d = r < p.n ? (p.rstate[r] & kPairsMask) : 0ull;
+        unsigned long long x = d;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wv] = x;
+        __syncthreads();
+        unsigned long long before = carry;
+        for (int v = 0; v < wv; ++v) before += ws[v];
+        const unsigned long long start = before + x - d;
+        if (r <= p.n) {
+            p.rbase[r] = start;
+            p.rec_off[r] = start;
+        }
+        __syncthreads();
+        if (tid == 1023) carry = start + d;
+        __syncthreads();
+    }
+}
+
+// Direct output: the pairs left in pk (lists whose record start was not yet known,
+// or that the table kernel counted) to their place; one workgroup per queue entry.
+__global__ __launch_bounds__(256) void canon_fallback_kernel(HParams p) {
+    const int64_t nq = (int64_t)*p.nfq;
+    for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const uint64_t src = p.fq[4 * q], c = p.fq[4 * q + 2], m = p.fq[4 * q + 3];
+        const uint64_t dst = p.rbase[p.fq[4 * q + 1]] + c;
+        for (uint64_t i = threadIdx.x; i < m; i += 256) {
+            const unsigned long long x = p.pk[src + i];
+            const uint32_t tag = (uint32_t)(x >> 62);
+            p.out_keys[dst + i] = unmix62(x & kM62);
+            p.out_counts[dst + i] = tag < 3u ? tag + 1u : p.pc[src + i];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
@@ -1376,6 +1639,14 @@ std::vector<HCache> h_ws;
 uint32_t h_claim_cap = kClaimW;
 uint32_t h_sort_cap = kSortCap;
 uint32_t h_sort_cap_big = kSortCapBig;
+int h_direct = 1;  // direct output when the caller's arrays hold every window (kmc_diag_canon_direct)
+constexpr int64_t kGroupLists = 8192;  // direct output: lists per launch of the common K4s instance (at least)
+#ifdef KMC_DIAG_HOOKS
+// the last direct-output call's fallback copies: queue entries, pairs (kmc_diag_canon_fallback)
+unsigned long long h_fb_entries = 0, h_fb_pairs = 0;
+std::vector<unsigned long long> h_fb_rec;  // fallback pairs per record
+unsigned long long h_fb_defer[3] = {0, 0, 0};  // lists queued: big instance, table (long / big's), table (common's)
+#endif
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1422,6 +1693,48 @@ extern "C" KMC_DIAG_API int kmc_diag_canon_sort_cap(unsigned cap) {
     h_sort_cap_big = cap == 0 ? 0u : kSortCapBig;  // 0: no counting sort at all (every list to the table)
     return KMC_OK;
 }
+
+// Test hook (diagnostic library only, not in kmc.h): 0 = the pairs always go
+// through pk and canon_place_kernel (the layout before round 5), 1 = direct output
+// whenever the caller's capacity holds every window (the default).
+extern "C" KMC_DIAG_API int kmc_diag_canon_direct(int on) {
+    if (on < 0 || on > 1) return KMC_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h_mu);
+    h_direct = on;
+    return KMC_OK;
+}
+
+// Test hook (diagnostic library only, not in kmc.h): the pairs of the last direct-
+// output call that went through pk and the fallback copy (their queue entries and
+// pairs), i.e. the lists that found their record's start unknown or counted in the
+// table kernel.
+extern "C" KMC_DIAG_API int kmc_diag_canon_fallback(unsigned long long *entries, unsigned long long *pairs) {
+    std::lock_guard<std::mutex> lk(h_mu);
+    *entries = h_fb_entries;
+    *pairs = h_fb_pairs;
+    return KMC_OK;
+}
+
+// Test hook (diagnostic library only): per record (up to cap) the fallback pairs of
+// the last direct-output call, and the lists queued to the big instance, the
+// table kernel's first and second launches.
+extern "C" KMC_DIAG_API int kmc_diag_canon_fallback_detail(unsigned long long *per_rec, unsigned cap,
+                                                            unsigned long long *queued3) {
+    std::lock_guard<std::mutex> lk(h_mu);
+    for (unsigned i = 0; i < cap && i < h_fb_rec.size(); ++i) per_rec[i] = h_fb_rec[i];
+    for (int j = 0; j < 3; ++j) queued3[j] = h_fb_defer[j];
+    return KMC_OK;
+}
+
+// Test hook (diagnostic library only, not in kmc.h): the longest list the big K4s
+// instance takes (0: none, so the lists above the common instance's cap go to the
+// table kernel); any value above kSortCapBig restores the default.  Call after
+// kmc_diag_canon_sort_cap, which resets it.
+extern "C" KMC_DIAG_API int kmc_diag_canon_sort_cap_big(unsigned cap) {
+    std::lock_guard<std::mutex> lk(h_mu);
+    h_sort_cap_big = cap > kSortCapBig ? kSortCapBig : cap;
+    return KMC_OK;
+}
 #endif
 
 namespace {
@@ -1437,7 +1750,7 @@ struct CanonPlan {
     std::vector<int2> fsplit;
     int64_t M = 0, Mc = 0, L = 0, windows = 0;
     size_t o_idx, o_lg, o_cb, o_ccb, o_w0, o_nw, o_lb, o_fs, o_cnt, o_off, o_cntc, o_offc, o_bs, o_ent, o_ls, o_pk,
-        o_pc, o_nd, o_do, o_err, o_dn, o_dl, o_bn, o_bl, total;
+        o_pc, o_nd, o_do, o_err, o_dn, o_dl, o_bn, o_bl, o_lrec, o_rst, o_rb, o_fq, o_nfq, o_d2n, o_d2l, total;
 };
 
 void canon_plan(const int64_t *hidx, int64_t n, int k, int cus, CanonPlan &P) {
@@ -1509,6 +1822,16 @@ void canon_plan(const int64_t *hidx, int64_t n, int k, int cus, CanonPlan &P) {
     P.o_dl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
     P.o_bn = o; o += al256(8);
     P.o_bl = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
+    // direct output (round 5)
+    P.o_lrec = o; o += al256((size_t)std::max<int64_t>(L, 1) * 4);
+    P.o_rst = o; o += al256((size_t)n * 8);
+    P.o_rb = o; o += al256((size_t)(n + 1) * 8);
+    // (at most two copies per list: its distinct slots' keys and its results; a
+    // list the table kernel counts has one)
+    P.o_fq = o; o += al256((size_t)std::max<int64_t>(L, 1) * 2 * 32);
+    P.o_nfq = o; o += al256(8);
+    P.o_d2n = o; o += al256(8);
+    P.o_d2l = o; o += al256((size_t)std::max<int64_t>(L, 1) * 24);
     P.total = o;
 }
 
@@ -1648,6 +1971,24 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     p.rec_off = rec_offsets;
     p.out_keys = keys;
     p.out_counts = counts;
+    int direct;
+    {
+        std::lock_guard<std::mutex> lk(h_mu);
+        direct = h_direct;
+    }
+    // direct output writes pairs before the total is known: only into arrays that
+    // hold every window (the distinct keys are at most that many)
+    direct = direct && keys && counts && capacity >= (uint64_t)P.windows;
+    p.direct = direct;
+    p.lrec = reinterpret_cast<int32_t *>(ws + P.o_lrec);
+    p.rstate = reinterpret_cast<unsigned long long *>(ws + P.o_rst);
+    p.rbase = reinterpret_cast<unsigned long long *>(ws + P.o_rb);
+    p.fq = reinterpret_cast<uint64_t *>(ws + P.o_fq);
+    p.nfq = reinterpret_cast<unsigned long long *>(ws + P.o_nfq);
+    p.defer2 = reinterpret_cast<uint64_t *>(ws + P.o_d2l);
+    p.ndefer2 = reinterpret_cast<unsigned long long *>(ws + P.o_d2n);
+    p.tq = p.defer;
+    p.ntq = p.ndefer;
     if ((he = hipMemcpyAsync((void *)p.idx, hidx.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.lg, lg.data(), n, hipMemcpyHostToDevice, stream)) ||
         (he = hipMemcpyAsync((void *)p.cbase, cbase.data(), (n + 1) * 8, hipMemcpyHostToDevice, stream)) ||
@@ -1659,8 +2000,10 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
                                     stream))))
         return (int)he;
     if ((he = hipMemsetAsync(p.err, 0, 4, stream)) || (he = hipMemsetAsync(p.ndefer, 0, 8, stream)) ||
-        (he = hipMemsetAsync(p.nbig, 0, 8, stream)))
+        (he = hipMemsetAsync(p.nbig, 0, 8, stream)) || (he = hipMemsetAsync(p.ndefer2, 0, 8, stream)))
         return (int)he;
+    if (direct)
+        hipLaunchKernelGGL(canon_direct_setup_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (M > 0) {
         if ((he = hipMemsetAsync(p.cnt, 0, (size_t)M * 4, stream)) ||
             (he = hipMemsetAsync(p.cnt_c, 0, (size_t)Mc * 4, stream)))
@@ -1672,18 +2015,92 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     launch_walk<WalkCoarse>(p, stream);
     hipLaunchKernelGGL(canon_list_start_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (NF > 0) hipLaunchKernelGGL(canon_fine_kernel, dim3((unsigned)NF), dim3(kWalkBlock), 0, stream, p);
+    const dim3 g_sort((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 2 * (int64_t)cus)));  // 2 per CU
+    const dim3 g_big((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (int64_t)cus)));       // 1 per CU
+    // the table kernel: two workgroups per CU (their tables fill the LDS) striding
+    // over the queued lists (count on the device); workgroups beyond it exit at once
+    const dim3 g_table((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (1024 / kCountBlock) * (int64_t)cus)));
+    if (direct) {
+        // the lists by length: the big instance's, in list order (a flag scan), and
+        // the ones too long for it, which the table kernel counts first
+        hipLaunchKernelGGL(canon_classify_kernel, dim3((unsigned)((L + 255) / 256)), dim3(256), 0, stream, p);
+        excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);
+        hipLaunchKernelGGL(canon_big_queue_kernel, dim3((unsigned)((L + 1 + 255) / 256)), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL(canon_table_kernel, g_table, dim3(kCountBlock), 0, stream, p);
+        // the common instance one group of records per launch: a group's lists find
+        // the start of their record known (every earlier record complete at the
+        // launch boundary) -- within one launch over every list, workgroups drift
+        // apart by more than a record's share of lists, and half of C4's pairs found
+        // their record's start unknown (scripts/canon_direct_probe.py).  A record
+        // with kGroupLists lists or more is a group of its own; smaller records are
+        // grouped up to that many lists (within such a group some lists take the pk
+        // path).
+        for (int64_t r0 = 0; r0 < n;) {
+            int64_t r1 = r0 + 1;
+            if (lbase[r1] - lbase[r0] < kGroupLists)
+                while (r1 < n && lbase[r1 + 1] - lbase[r0] <= kGroupLists && lbase[r1 + 1] - lbase[r1] < kGroupLists)
+                    ++r1;
+            HParams pg = p;
+            pg.l_lo = lbase[r0];
+            pg.l_hi = lbase[r1];
+            // the group's long lists (big instance) first, then the others; a group
+            // whose records are shorter than the common instance's cap has none
+            int64_t wmax = 0;
+            for (int64_t r = r0; r < r1; ++r) wmax = std::max<int64_t>(wmax, hidx[r + 1] - hidx[r] - k);
+            if (wmax > (int64_t)p.sort_cap)
+                hipLaunchKernelGGL(canon_sort_big_kernel<true>, g_big, dim3(SortBig::kBlock), 0, stream, pg);
+            const dim3 gg((unsigned)std::max<int64_t>(1, std::min<int64_t>(pg.l_hi - pg.l_lo, 2 * (int64_t)cus)));
+            hipLaunchKernelGGL(canon_sort_kernel<true>, gg, dim3(kSortBlock), 0, stream, pg);
+            r0 = r1;
+        }
+        HParams p2 = p;  // the common instance's deferrals
+        p2.tq = p.defer2;
+        p2.ntq = p.ndefer2;
+        hipLaunchKernelGGL(canon_table_kernel, g_table, dim3(kCountBlock), 0, stream, p2);
+        hipLaunchKernelGGL(canon_direct_final_kernel, dim3(1), dim3(1024), 0, stream, p);
+        hipLaunchKernelGGL(canon_fallback_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 4096))),
+                           dim3(256), 0, stream, p);
+        uint64_t distinct = 0;
+        uint32_t err = 0;
+        if ((he = hipGetLastError()) ||
+            (he = hipMemcpyAsync(&distinct, p.rbase + n, 8, hipMemcpyDeviceToHost, stream)) ||
+            (he = hipMemcpyAsync(&err, p.err, 4, hipMemcpyDeviceToHost, stream)) ||
+            (he = hipStreamSynchronize(stream)))
+            return (int)he;
+        if (err) return KMC_ERR_INVALID_ARG;  // a record far beyond any genome (see kMaxPasses)
+        *num_distinct = distinct;
+#ifdef KMC_DIAG_HOOKS
+        {
+            unsigned long long ne = 0;
+            if ((he = hipMemcpy(&ne, p.nfq, 8, hipMemcpyDeviceToHost))) return (int)he;
+            std::vector<uint64_t> q(4 * ne);
+            if (ne && (he = hipMemcpy(q.data(), p.fq, 32 * ne, hipMemcpyDeviceToHost))) return (int)he;
+            unsigned long long np = 0;
+            std::vector<unsigned long long> per(n, 0);
+            for (unsigned long long i = 0; i < ne; ++i) {
+                np += q[4 * i + 3];
+                per[q[4 * i + 1]] += q[4 * i + 3];
+            }
+            unsigned long long dq[3] = {0, 0, 0};
+            if ((he = hipMemcpy(&dq[0], p.nbig, 8, hipMemcpyDeviceToHost)) ||
+                (he = hipMemcpy(&dq[1], p.ndefer, 8, hipMemcpyDeviceToHost)) ||
+                (he = hipMemcpy(&dq[2], p.ndefer2, 8, hipMemcpyDeviceToHost)))
+                return (int)he;
+            std::lock_guard<std::mutex> lk(h_mu);
+            h_fb_entries = ne;
+            h_fb_pairs = np;
+            h_fb_rec.swap(per);
+            for (int j = 0; j < 3; ++j) h_fb_defer[j] = dq[j];
+        }
+#endif
+        return KMC_OK;
+    }
     // persistent, two workgroups per CU (64 KB of LDS each), striding over the lists
-    hipLaunchKernelGGL(canon_sort_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, 2 * (int64_t)cus))),
-                       dim3(kSortBlock), 0, stream, p);
-    // the lists it handed to its big instance (one 1 024-thread workgroup per CU;
-    // workgroups beyond their number exit at once), before the table kernel, which
-    // also takes the big instance's deferrals
-    hipLaunchKernelGGL(canon_sort_big_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (int64_t)cus))),
-                       dim3(SortBig::kBlock), 0, stream, p);
-    // the deferred lists (count on the device): two workgroups per CU (their tables
-    // fill the LDS) striding over them; workgroups beyond the count exit at once
-    hipLaunchKernelGGL(canon_table_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(L, (1024 / kCountBlock) * (int64_t)cus))),
-                       dim3(kCountBlock), 0, stream, p);
+    hipLaunchKernelGGL(canon_sort_kernel<false>, g_sort, dim3(kSortBlock), 0, stream, p);
+    // the lists it handed to its big instance (workgroups beyond their number exit at
+    // once), before the table kernel, which also takes the big instance's deferrals
+    hipLaunchKernelGGL(canon_sort_big_kernel<false>, g_big, dim3(SortBig::kBlock), 0, stream, p);
+    hipLaunchKernelGGL(canon_table_kernel, g_table, dim3(kCountBlock), 0, stream, p);
     excl_scan_u32(p.ndist, L, bsum, p.dist_off, stream);
     hipLaunchKernelGGL(canon_recoff_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
     uint64_t distinct = 0;

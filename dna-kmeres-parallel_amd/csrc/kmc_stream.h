@@ -14,19 +14,15 @@
 
 #include <cstdint>
 
+namespace kmc {
+
 // Tiles kept in flight per wave ahead of the one being counted, and whether the
 // once-read sequence stream uses non-temporal (nt) loads: defaults of the dense
 // histogram kernels (round 2, same-box A/B: PF 2 -> 3 and nt loads took k = 8 from
 // 2.32 to 2.24 ms and k = 1..7 down 2-4 %; profiles/r02_stream_pf_nt_ab.txt); the
 // radix walks pass their own (PF 2, plain loads: PF 3 + nt made C3 4 % slower).
-#ifndef KMC_PF
-#define KMC_PF 3
-#endif
-#ifndef KMC_NT
-#define KMC_NT 1
-#endif
-
-namespace kmc {
+constexpr int kStreamPF = 3;
+constexpr int kStreamNT = 1;
 
 constexpr int kTileShift = 10;  // 1 KiB per wave per tile
 constexpr int kTile = 1 << kTileShift;
@@ -81,13 +77,9 @@ __device__ __forceinline__ uint4 load_lane(const char *__restrict__ data, int64_
     const int64_t base = t << kTileShift;
     const int64_t q = base + (int64_t)lane * 16;
     if (base >= rl && base + kTile <= rh) {  // wave-uniform: whole tile readable
-#if KMC_NT
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
         const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(data + q));
         return make_uint4(x[0], x[1], x[2], x[3]);
-#else
-        return *reinterpret_cast<const uint4 *>(data + q);
-#endif
     }
     uint32_t v[4] = {0u, 0u, 0u, 0u};
     if (q >= rl && q + 16 <= rh) {
@@ -247,7 +239,7 @@ __device__ __forceinline__ int64_t tile_base(int64_t t, int64_t rl) {
     return b > rl16 ? b : rl16;
 }
 
-template <int NT = KMC_NT>
+template <int NT = kStreamNT>
 __device__ __forceinline__ uint4 load_tile_fast(__amdgpu_buffer_rsrc_t rsrc, int64_t base_off, int64_t t,
                                                 int lane) {
     const int64_t off = (t << kTileShift) - base_off + (int64_t)lane * 16;
@@ -286,14 +278,14 @@ __device__ __forceinline__ uint4 mask_range(uint4 v, int64_t q, int64_t rl, int6
 // op.after_iter, so workgroup barriers inside it stay matched).  Tile t+1 is
 // decoded while tile t is counted (it is lane 63's halo of t).
 //
-// Prefetch: KMC_PF tiles ahead, in a ring of KMC_PF+1 register slots whose index
+// Prefetch: PF tiles ahead, in a ring of PF+1 register slots whose index
 // is a compile-time constant in every step (the loop is unrolled by the ring
 // size), issued unconditionally (load_tile_fast) so that no branch merges pending
 // and completed loads.  Both matter: register moves between slots (r[q] =
 // r[q+1]) or a load inside a branch make the compiler wait for the load it has
 // just issued (s_waitcnt vmcnt(0)) before the next decode, which leaves one tile
-// in flight per wave whatever KMC_PF says.
-template <int K, int PF_ = KMC_PF, int NT_ = KMC_NT>
+// in flight per wave whatever PF says.
+template <int K, int PF_ = kStreamPF, int NT_ = kStreamNT>
 struct TileStream {
     static constexpr int PF = PF_;
     static constexpr int NT = NT_;
@@ -365,7 +357,7 @@ struct TileStream {
     }
 };
 
-template <int K, class Op, int PF = KMC_PF, int NT = KMC_NT>
+template <int K, class Op, int PF = kStreamPF, int NT = kStreamNT>
 __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int64_t t0, int64_t t1, int64_t per,
                                              int64_t ps, int64_t pe, int64_t rl, int64_t rh, int lane, Op &op) {
     using TS = TileStream<K, PF, NT>;

@@ -73,7 +73,8 @@ class diag:
     """Context manager: inside it every binding calls lib/libkmc_diag.so, the same
     library built with the test hooks (kmc_diag_radix_mode, kmc_diag_canon_claim_cap,
     kmc_diag_canon_sort_cap, kmc_diag_dense_spill_cap) that force an algorithm
-    choice; libkmc.so exports none of them.  `with kmc.diag() as D: D.kmc_diag_...`"""
+    choice (kmc_diag_canon_sort_cap_big, kmc_diag_canon_direct too); libkmc.so
+    exports none of them.  `with kmc.diag() as D: D.kmc_diag_...`"""
 
     def __enter__(self):
         global _diag_lib, _active
@@ -82,6 +83,11 @@ class diag:
             _diag_lib.kmc_diag_radix_mode.argtypes = [ctypes.c_int, ctypes.c_float]
             _diag_lib.kmc_diag_canon_claim_cap.argtypes = [ctypes.c_uint]
             _diag_lib.kmc_diag_canon_sort_cap.argtypes = [ctypes.c_uint]
+            _diag_lib.kmc_diag_canon_sort_cap_big.argtypes = [ctypes.c_uint]
+            _diag_lib.kmc_diag_canon_direct.argtypes = [ctypes.c_int]
+            _diag_lib.kmc_diag_canon_fallback.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)] * 2
+            _diag_lib.kmc_diag_canon_fallback_detail.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_uint,
+                                                                 ctypes.POINTER(ctypes.c_ulonglong)]
             _diag_lib.kmc_diag_dense_spill_cap.argtypes = [ctypes.c_uint]
         self._prev = _active
         _active = _diag_lib
@@ -93,7 +99,8 @@ class diag:
         # restore the defaults for the next user of the diagnostic library
         L.kmc_diag_radix_mode(0, 1.0)
         L.kmc_diag_canon_claim_cap(0)
-        L.kmc_diag_canon_sort_cap(1 << 30)
+        L.kmc_diag_canon_sort_cap(1 << 30)  # (also restores the big instance's cap)
+        L.kmc_diag_canon_direct(1)
         L.kmc_diag_dense_spill_cap(0)
         _active = self._prev
         return False

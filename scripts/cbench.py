@@ -250,9 +250,15 @@ def main():
     ap.add_argument("--cpu-sample-c3", type=int, default=2_000_000, help="bases per CPU thread (0 = skip)")
     ap.add_argument("--cpu-sample-c4", type=int, default=16_000_000, help="bases per CPU thread (0 = skip)")
     ap.add_argument("--no-check", dest="check", action="store_false", help="skip the parity checks")
+    ap.add_argument("--canon-direct", type=int, default=None,
+                    help="A/B of the canonical output path through the diagnostic library: 1 = direct output "
+                         "(the default), 0 = pk + place copy (the layout before round 5)")
     a = ap.parse_args()
     import torch
     import kmc
+    if a.canon_direct is not None:
+        D = kmc.diag().__enter__()  # every binding calls lib/libkmc_diag.so from here on
+        assert D.kmc_diag_canon_direct(a.canon_direct) == 0
     dev = torch.device("cuda:0")
     cfgs = a.configs.split(",")
     if "c1" in cfgs:
@@ -333,6 +339,8 @@ def main():
         line = {"config": cfg.upper(), "k": k, "records": len(lens), "bases": sum(lens), "windows": kmers,
                 "valid_windows": tot, "distinct": int(keys.numel()), "s_med": med, "s_min": best,
                 "kmers_per_s": kmers / med, "alg_bytes": alg, "GBps": alg / med / 1e9, "frac8TB": alg / med / 8e12}
+        if a.canon_direct is not None:
+            line["canon_direct"] = a.canon_direct
         line.update(extra)
         line["max_count"] = int(counts.max().item())
         line["keys_count_gt1"] = int((counts > 1).sum().item())

@@ -133,27 +133,32 @@ def test_canonical_pass_overflow_split(kmc, oracle, cuda, cap):
             assert_same(gpu_canon(kmc, cuda, data, idx, k), oracle.count_canonical(data, idx, k), "cap=%d k=%d" % (cap, k))
 
 
-@pytest.mark.parametrize("scap", [0, 1, 2500, 1 << 30])
-def test_canonical_sort_and_table_paths(kmc, oracle, cuda, scap):
-    """Lists split between the counting-sort kernel (K4s: lists of at most scap keys,
-    no key more than 16 times in one of its slots) and the probed table kernel
-    (every other list): the same counts whatever the split.  Records with lists of
-    ~2-4 K keys, hot keys (a list deferred from K4s for a crowded slot), short
-    records (lists of a few keys)."""
-    import ctypes
+@pytest.mark.parametrize("scap,big", [(0, None), (1, 0), (2500, 0), (1, None), (2500, None), (1 << 30, None)])
+def test_canonical_sort_and_table_paths(kmc, oracle, cuda, scap, big):
+    """Lists split between the three counting kernels by the diagnostic hooks: the
+    common K4s instance takes lists of at most `scap` keys (0: none), the big K4s
+    instance those up to `big` keys (None: its default 12 288; 0: none) and the
+    probed table kernel the rest (and any list with too many crowded slots) -- the
+    same counts whatever the split: (0, -) every list in the table kernel; (1 or
+    2500, 0) common + table; (1 or 2500, default) common + big (lists of 2 .. 12 288
+    keys in the big instance); (default, default) the shipped split.  Records with
+    lists of ~2-4 K keys, hot keys (a list deferred from K4s for a crowded slot),
+    short records (lists of a few keys)."""
     rng = np.random.default_rng(5 + scap % 97)
     data, idx = random_records(rng, [1_200_000, 9000, 40, 700_001], b"ACGTNacgt",
                                (.2, .2, .2, .2, .04, .04, .04, .04, .04))
     rep = np.frombuffer(b"ACGTTGCAAT" * 3000 + b"G" * 900 + b"ACGATCGATCGGA" * 400, dtype=np.uint8)
     data = np.concatenate([data, rep, np.zeros(1, np.uint8)])
     idx = np.append(idx, data.size)
-    with kmc.diag() as D:  # the hook lives in the diagnostic library only
+    with kmc.diag() as D:  # the hooks live in the diagnostic library only
         assert D.kmc_diag_canon_sort_cap(scap) == 0
+        if big is not None:
+            assert D.kmc_diag_canon_sort_cap_big(big) == 0
         for k in (17, 31):
             for flags in (0, kmc.CANON_SOFTMASK):
                 got = gpu_canon(kmc, cuda, data, idx, k, flags)
                 exp = oracle.count_canonical(data, idx, k, soft=bool(flags & 1))
-                assert_same(got, exp, "scap=%d k=%d flags=%d" % (scap, k, flags))
+                assert_same(got, exp, "scap=%d big=%s k=%d flags=%d" % (scap, big, k, flags))
 
 
 def test_canonical_crowded_list_deferred(kmc, oracle, cuda):
@@ -328,6 +333,37 @@ def test_canonical_big_lists_sort_vs_table(kmc, cuda):
             assert torch.equal(gk, rk) and torch.equal(gc, rc), "k=%d record %d" % (k, s)
         assert int(got[0][1].to(torch.int64).sum()) == L - k + 1
         assert int(got[1][1].to(torch.int64).sum()) == 60_000_000 - k + 1
+
+
+@pytest.mark.parametrize("k,soft", [(31, True), (21, False), (13, True)])
+def test_canonical_direct_output_vs_pk_layout(kmc, oracle, cuda, k, soft):
+    """Direct output (round 5: the pairs written by the counting kernels straight
+    to their record's region when its start is known, else through pk and the
+    fallback copy) against the pk + place layout (kmc_diag_canon_direct(0)) and the
+    self-oracle: the same per-record sets and the same record offsets, on a
+    repeat-rich genome (lists whose failing slots overflow the LDS staging, crowded
+    slots) beside random records, many short ones and empty ones."""
+    import os
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import genome_synth
+    rng = np.random.default_rng(700 + k)
+    g, gi, _, _ = genome_synth.repeat_genome(torch, cuda, 0.02, seed=k, min_len=20_000)
+    gh, gih = g.cpu().numpy(), gi.cpu().numpy()
+    d2, i2 = random_records(rng, [0, 5, 250_000, 1, 31, 32, 9000] + list(rng.integers(0, 300, size=500)),
+                            b"ACGTNacgt", (.2, .2, .2, .2, .04, .04, .04, .04, .04))
+    data = np.concatenate([gh, d2])
+    idx = np.concatenate([gih, gih[-1] + i2[1:]]).astype(np.int64)
+    flags = kmc.CANON_SOFTMASK if soft else 0
+    exp = oracle.count_canonical(data, idx, k, soft=soft)
+    got = {}
+    with kmc.diag() as D:
+        for mode in (1, 0):
+            assert D.kmc_diag_canon_direct(mode) == 0
+            got[mode] = gpu_canon(kmc, cuda, data, idx, k, flags)
+            assert_same(got[mode], exp, "direct=%d k=%d soft=%s" % (mode, k, soft))
+    np.testing.assert_array_equal(got[0][2], got[1][2])
 
 
 def test_canonical_capacity_error(kmc, cuda):
