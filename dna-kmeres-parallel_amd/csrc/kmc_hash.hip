@@ -50,21 +50,6 @@
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
-#ifndef KMC_CANON_PASS
-#define KMC_CANON_PASS 2048
-#endif
-#ifndef KMC_CANON_RES
-#define KMC_CANON_RES 16
-#endif
-// K1 / K3a: the next chunk's 48 bytes loaded before the current chunk is hashed (1)
-#ifndef KMC_WALK_PF
-#define KMC_WALK_PF 1
-#endif
-// K3b: the next round's entries loaded before the current round is ranked (1)
-#ifndef KMC_FINE_PF
-#define KMC_FINE_PF 1
-#endif
-
 namespace kmc {
 namespace {
 
@@ -75,29 +60,17 @@ constexpr int kCoarseLg = 7;                 // at most 128 coarse buckets per r
 constexpr int kMaxBk = 1 << (kMaxLg - kCoarseLg);  // buckets of one staged round (coarse, or lists per bucket)
 constexpr int64_t kListTarget = 4096;        // windows per list aimed at
 constexpr int kRound = 16 * kWalkBlock;      // K3a / K3b windows per staged round
-#ifndef KMC_CANON_BLOCK
-#define KMC_CANON_BLOCK 512
-#endif
-#ifndef KMC_CANON_TLG
-#define KMC_CANON_TLG 12
-#endif
-constexpr int kCountBlock = KMC_CANON_BLOCK;  // K4 threads per workgroup (1024 / kCountBlock workgroups per CU)
-constexpr int kTableLg = KMC_CANON_TLG;
+constexpr int kCountBlock = 512;  // K4 threads per workgroup (1024 / kCountBlock workgroups per CU)
+constexpr int kTableLg = 12;
 constexpr int kTableSlots = 1 << kTableLg;   // K4 LDS table: 4 096 x (8 + 4) B, double hashing
 constexpr int kWaves4 = kCountBlock / 64;
-#ifndef KMC_CANON_STAGE
-#define KMC_CANON_STAGE 320
-#endif
-constexpr int kStage = KMC_CANON_STAGE;                // K4 per-wave keys staged for one probe loop
-#ifndef KMC_CANON_CLAIMW
-#define KMC_CANON_CLAIMW 320
-#endif
-constexpr int kClaimW = KMC_CANON_CLAIMW;      // K4 per-wave claims per pass (2-byte slot ids)
+constexpr int kStage = 320;                  // K4 per-wave keys staged for one probe loop
+constexpr int kClaimW = 320;                 // K4 per-wave claims per pass (2-byte slot ids)
 constexpr uint32_t kMaxInitPasses = 16;
 constexpr int kPassTop = 64 - kMaxLg;          // pass bits [kPassTop - log2 P, kPassTop), below the list bits
 constexpr uint32_t kMaxPasses = 1u << (kPassTop - 32);
-constexpr int kPassDistinct = KMC_CANON_PASS;  // keys per K4 pass aimed at (table load <= 0.47)
-constexpr int kRes = KMC_CANON_RES;            // K4 keys per thread held in registers
+constexpr int kPassDistinct = 2048;          // keys per K4 pass aimed at (table load <= 0.47)
+constexpr int kRes = 16;                     // K4 keys per thread held in registers
 constexpr int64_t kResKeys = (int64_t)kRes * kCountBlock;
 static_assert(kPassDistinct <= kWaves4 * kClaimW && kTableSlots < 65536 , "K4 sizes");
 
@@ -225,7 +198,7 @@ __device__ __forceinline__ void chunk_codes(uint4 r, bool soft, uint32_t &code, 
 // record piece [ps, pe) (window starts) of a record whose terminator is at
 // rend - 1: bit j of the result is set when h[j] holds window q + j.
 // The 48 bytes chunk_keys decodes for chunk q (its 16 window starts + 32 halo bytes),
-// loaded ahead of use by the input walks (KMC_WALK_PF)
+// loaded ahead of use by the input walks
 struct ChunkRaw {
     uint4 r[3];
 };
@@ -379,12 +352,11 @@ __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
         __syncthreads();
         const int64_t qs = (int64_t)kWalkBlock << 4;
         int64_t q = ((ps >> 4) + threadIdx.x) << 4;
-        ChunkRaw nx;
-        if (KMC_WALK_PF) nx = chunk_raw(p, q);  // (unconditional: past the piece it reads harmlessly)
+        ChunkRaw nx = chunk_raw(p, q);  // (unconditional: past the piece it reads harmlessly)
         for (; q < pe; q += qs) {
             unsigned long long h[16];
-            const ChunkRaw cr = KMC_WALK_PF ? nx : chunk_raw(p, q);
-            if (KMC_WALK_PF) nx = chunk_raw(p, q + qs);  // the next chunk, in flight
+            const ChunkRaw cr = nx;
+            nx = chunk_raw(p, q + qs);  // the next chunk, in flight
             const uint32_t vm = chunk_keys<FWD, BIGK>(p, cr, q, ps, pe, rend, h);
             const uint32_t dummy = kK1Dummy + (threadIdx.x & 63u);
 #pragma unroll
@@ -489,10 +461,7 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
 // taking more than RING - 7 of a round's entries: skewed input) go straight to
 // their position in a cold path.  nbk = 2^lgb <= kMaxBk.
 constexpr int kRingEnt = 16384;  // 8-byte ring entries in LDS (128 KB)
-#ifndef KMC_K3B_SEG
-#define KMC_K3B_SEG 16
-#endif
-constexpr uint32_t kSeg = KMC_K3B_SEG;  // entries per HBM segment: 8 (64 bytes) or 16 (a whole 128-byte line)
+constexpr uint32_t kSeg = 16;  // entries per HBM segment: a whole 128-byte line (8, 64 bytes, until round 4)
 static_assert(kSeg == 8 || kSeg == 16, "K3b segments");
 struct Ring8Lds {
     unsigned long long ring[kRingEnt];
@@ -660,16 +629,13 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
         uint64_t *dst = lg > lgc ? p.ent_c : p.ent;
         const auto bk = [lgc](unsigned long long x) { return top_bits(x, lgc); };
         const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
-        ChunkRaw nx;
-        if (KMC_WALK_PF) nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
+        ChunkRaw nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
         for (int64_t cb = c0; cb < c1; cb += kWalkBlock) {
             const int64_t c = cb + threadIdx.x;
             unsigned long long h[16];
-            uint32_t vm = 0u;
-            ChunkRaw cr = nx;
-            if (!KMC_WALK_PF) cr = chunk_raw(p, c << 4);
-            if (KMC_WALK_PF) nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
-            vm = chunk_keys<FWD, BIGK>(p, cr, c << 4, ps, pe, rend, h);  // (past the piece: vm = 0, h defined)
+            const ChunkRaw cr = nx;
+            nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
+            const uint32_t vm = chunk_keys<FWD, BIGK>(p, cr, c << 4, ps, pe, rend, h);  // (past the piece: vm = 0, h defined)
             if (lg > lgc)
                 staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return x; }, dst);
             else  // buckets are the lists
@@ -714,7 +680,7 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
     rg.init(&R, p.ent, lf, p.list_start[lb + (threadIdx.x >> (10 - lf))]);
     __syncthreads();
     // the next round's entries are loaded before this round is ranked and flushed
-    // (KMC_FINE_PF; one workgroup per CU whose waves meet at every round's barriers
+    // (one workgroup per CU whose waves meet at every round's barriers
     // would otherwise wait on HBM once per round)
     unsigned long long xn[8];
     const auto fetch = [&](uint64_t i0) {
@@ -724,14 +690,13 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
             xn[j] = i < a1 ? p.ent_c[i] : 0ull;
         }
     };
-    if (KMC_FINE_PF) fetch(a0);
+    fetch(a0);
     for (uint64_t i0 = a0; i0 < a1; i0 += 8 * kWalkBlock) {
         unsigned long long v[8], x[8];
         uint32_t bk[8], vm = 0u;
-        if (!KMC_FINE_PF) fetch(i0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = xn[j];
-        if (KMC_FINE_PF && i0 + 8 * kWalkBlock < a1) fetch(i0 + 8 * kWalkBlock);
+        if (i0 + 8 * kWalkBlock < a1) fetch(i0 + 8 * kWalkBlock);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
@@ -1099,13 +1064,7 @@ using SortBig = SortCfg<1024, 12, kSortCapBigCfg, 13, 15232, 2048>;   // LDS: 1 
 constexpr int kSortBlock = SortSmall::kBlock;
 constexpr uint32_t kSortCap = SortSmall::kCap;
 constexpr uint32_t kSortCapBig = SortBig::kCap;
-#ifndef KMC_K4S_PF
-#define KMC_K4S_PF 1
-#endif
-#ifndef KMC_SORT_MAXM
-#define KMC_SORT_MAXM 8
-#endif
-constexpr uint32_t kSortMaxM = KMC_SORT_MAXM;         // keys per slot handled by the pairwise dedup
+constexpr uint32_t kSortMaxM = 8;                     // keys per slot handled by the pairwise dedup
 constexpr uint32_t kHotMax = 128;                     // crowded slots per list handled by wave rounds
 
 template <class C>
@@ -1205,7 +1164,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
     // rank adds and the scatter's slot reads all before their first use, and one
     // output reservation per wave, measured no further change and was not kept.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), gfx9 encoding
-    if (KMC_K4S_PF && nxt) {
+    if (nxt) {
         // (round 4) the workgroup's next list [nb0, ne0) touched once per 128-byte
         // line now, so that its key loads above find it in L2 / MALL one list later
         // (same box: K4s 15.1 -> 14.5 ms on C4).  An LDS-DMA dword per line into a
@@ -1510,23 +1469,21 @@ __global__ __launch_bounds__(SortBig::kBlock) void canon_sort_big_kernel(HParams
 }
 
 // K5: pairs to their final place; record offsets.  Four loads in flight per thread
-// (KMC_PLACE_U; 1 and 8 measured, and non-temporal loads / stores: C4R place 9.4 / 8.1 ms against 8.3, C4 within the
+// (1 and 8 measured, and non-temporal loads / stores: C4R place 9.4 / 8.1 ms against 8.3, C4 within the
 // box noise; four consecutive pairs per thread with 16-byte stores: no gain either).
-#ifndef KMC_PLACE_U
-#define KMC_PLACE_U 4
-#endif
+constexpr int kPlaceU = 4;
 __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
     const int64_t l = blockIdx.x;
     const uint64_t src = p.list_start[l], dst = p.dist_off[l], m = p.ndist[l];
-    for (uint64_t i0 = threadIdx.x; i0 < m; i0 += 256 * KMC_PLACE_U) {
-        unsigned long long x[KMC_PLACE_U];
+    for (uint64_t i0 = threadIdx.x; i0 < m; i0 += 256 * kPlaceU) {
+        unsigned long long x[kPlaceU];
 #pragma unroll
-        for (int u = 0; u < KMC_PLACE_U; ++u) {
+        for (int u = 0; u < kPlaceU; ++u) {
             const uint64_t i = i0 + 256u * u;
             x[u] = i < m ? p.pk[src + i] : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < KMC_PLACE_U; ++u) {
+        for (int u = 0; u < kPlaceU; ++u) {
             const uint64_t i = i0 + 256u * u;
             if (i < m) {
                 const uint32_t tag = (uint32_t)(x[u] >> 62);

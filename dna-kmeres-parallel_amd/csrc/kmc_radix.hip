@@ -42,55 +42,24 @@
 #include "kmc_scan.h"
 #include "kmc_stream.h"
 
-// tile prefetch depth and nt loads of the count (R1) and scatter (R3) walks, each
-// from a same-box A/B: R1 PF 3 + nt 2.04-2.06 -> 1.95-2.01 ms; R3 PF 2-4 equal, and
-// nt loads made it slower
-#ifndef KMC_RSCAT_PF
-#define KMC_RSCAT_PF 2
-#endif
-#ifndef KMC_RCOUNT_PF
-#define KMC_RCOUNT_PF 3
-#endif
-#ifndef KMC_RCOUNT_NT
-#define KMC_RCOUNT_NT 1
-#endif
-#ifndef KMC_R4_U
-#define KMC_R4_U 4  // R4 16-byte entry loads in flight per lane (2 / 4 / 8 measured equal, same box)
-#endif
-#ifndef KMC_RING_RT
-#define KMC_RING_RT 1
-#endif
-// R3 ring addressing when a ring is 64 entries (k = 13): 1 = circular (list index
-// g in slot (g mod 64) ^ swz, so the partial last segment stays in place: no tail
-// move in the flush), 0 = rebased every round (the partial segment copied to the
-// ring's start).  Round 4, same box (profiles/r04b_r3_variants.txt): R3 8.78-8.83
-// -> 8.34-8.40 ms, C3 14.59-14.65 -> 14.14-14.18 ms.  (Reading a segment's chunks
-// only when the quad stores one, instead of unconditionally, made R3 24 ms: the
-// flush is latency-bound, and the predicated reads serialised it.)
-#ifndef KMC_RING_CIRC
-#define KMC_RING_CIRC 1
-#endif
-// R4 list end: 1 = one pass over the LDS bins that writes the stage row, sums the
-// bins (wrap check) and clears them for the next list; 0 = a sum pass, a write
-// pass and a clear pass.  Round 4, same box: R4 4.34 -> 4.19 ms.
-#ifndef KMC_R4_FUSE
-#define KMC_R4_FUSE 1
-#endif
-
 namespace kmc {
 namespace {
 
+// Tile prefetch depth and nt loads of the count (R1) and scatter (R3) walks, each
+// from a same-box A/B: R1 PF 3 + nt 2.04-2.06 -> 1.95-2.01 ms; R3 PF 2-4 equal, and
+// nt loads made it slower.
+constexpr int kRScatPF = 2, kRCountPF = 3, kRCountNT = 1;
+// R4: 16-byte entry loads in flight per lane (2 / 4 / 8 measured equal, same box)
+constexpr int kR4U = 4;
+
 // Low code bits resolved by the per-list LDS histogram (2^low bins, at most
 // 128 KB); the rest select the bucket.  At least 64 buckets per record, so the
-// bucket counters of R1/R3 see few same-address LDS atomics.
-#ifndef KMC_RADIX_LOW_MAX
-#define KMC_RADIX_LOW_MAX 16
-#endif
-// (16 low bits — two 16-bit R4 bins per LDS word — from k = 12 on: half the
-// buckets, so R3's runs per bucket and round are twice as long; at k = 11 the
-// 64 buckets per record would leave R4 too few workgroups)
+// bucket counters of R1/R3 see few same-address LDS atomics.  16 low bits -- two
+// 16-bit R4 bins per LDS word -- from k = 12 on: half the buckets, so R3's runs
+// per bucket and round are twice as long; at k = 11 the 64 buckets per record
+// would leave R4 too few workgroups.
 __host__ __device__ constexpr int low_bits(int k) {
-    return 2 * k - 6 < (k >= 12 ? KMC_RADIX_LOW_MAX : 15) ? 2 * k - 6 : (k >= 12 ? KMC_RADIX_LOW_MAX : 15);
+    return 2 * k - 6 < (k >= 12 ? 16 : 15) ? 2 * k - 6 : (k >= 12 ? 16 : 15);
 }
 
 struct RParams {
@@ -232,7 +201,7 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
         if constexpr (SAMPLE) {
             sample_tiles<K>(p.data, a0, a1, ps, pe, g.rl, g.rh, lane, (uint32_t)(w * 16 + wave) ^ (uint32_t)s, op);
         } else {
-            stream_tiles<K, RCountOp<K>, KMC_RCOUNT_PF, KMC_RCOUNT_NT>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+            stream_tiles<K, RCountOp<K>, kRCountPF, kRCountNT>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         }
         __syncthreads();
         for (int b = tid; b < NBK; b += BLOCK) {
@@ -320,7 +289,7 @@ struct RingGeom {
     static constexpr int RING = 65536 / NBK;    // entries per bucket ring (128 KB in all)
     static_assert(NBK <= BLOCK && RING >= 64 && (RING & (RING - 1)) == 0, "ring geometry");
     // the fill (in bytes) of one round stays below 2^16: it cannot carry into the ring field
-    static_assert(2 * (BLOCK * 16 * KMC_RING_RT + 32) < 65536, "one tile per wave per round");
+    static_assert(2 * (BLOCK * 16 + 32) < 65536, "one tile per wave per round");
 };
 
 // slot swizzle of bucket b (XOR mask, a multiple of 8 slots below 64)
@@ -332,7 +301,14 @@ __device__ __forceinline__ uint32_t ring_word(uint32_t b, uint32_t f0) {
     return ((b * (uint32_t)RingGeom<K>::RING | ring_swz(b)) << 16) | (f0 << 1);
 }
 
-// circular ring (KMC_RING_CIRC, RING = 64): the round's entries start at list index
+// circular ring (RING = 64, k = 13): list index g in slot (g mod 64) ^ swz, so the
+// partial last segment stays in place (no tail move in the flush; the other
+// geometries rebase the ring every round, the partial segment copied to its
+// start).  Round 4, same box (profiles/r04b_r3_variants.txt): R3 8.78-8.83 ->
+// 8.34-8.40 ms, C3 14.59-14.65 -> 14.14-14.18 ms.  (Reading a segment's chunks
+// only when the quad stores one, instead of unconditionally, made R3 24 ms: the
+// flush is latency-bound, and the predicated reads serialised it.)
+// The round's entries start at list index
 // f (relative to the piece's 32-aligned base); its first segment h = f & ~31 lives
 // in ring half (h & 32), which is folded into the swizzle: with x = (f & 31) + rank
 // < 64, (h + x) mod 64 = x ^ (h & 32)
@@ -341,7 +317,7 @@ __device__ __forceinline__ uint32_t ring_word_circ(uint32_t b, uint32_t f) {
     return ((b * (uint32_t)RingGeom<K>::RING | (ring_swz(b) ^ (f & 32u))) << 16) | ((f & 31u) << 1);
 }
 template <int K>
-constexpr bool ring_circ() { return KMC_RING_CIRC && RingGeom<K>::RING == 64; }
+constexpr bool ring_circ() { return RingGeom<K>::RING == 64; }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
@@ -366,7 +342,6 @@ struct RRingOp {
     uint32_t f, v;
     uint32_t f0;           // f at the piece start (the piece's entries: f - f0)
     uint32_t cap;          // end of the region (relative to P0; ~0: exact offsets)
-    int held = 0;          // tiles of this round taken (workgroup-uniform)
     // sampled mode: this workgroup's overflow list and its LDS counter; stage index
     // of the piece's record
     unsigned long long *ovf;
@@ -548,9 +523,7 @@ struct RRingOp {
         par ^= 1u;
     }
 
-    __device__ void after_iter(int64_t i, int64_t per, bool) {
-        if (++held < KMC_RING_RT && i + 1 < per) return;
-        held = 0;
+    __device__ void after_iter(int64_t, int64_t, bool) {  // one tile per wave per round
         lds_barrier();  // every window of the round is ranked and in its ring
         flush();
         lds_barrier();  // rings read, W set up: the next round may write
@@ -637,7 +610,7 @@ __global__ __launch_bounds__(1024) void radix_ring_kernel(RParams p) {
         const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
         const int64_t a0 = tp0 + (int64_t)wave * per;
         const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-        stream_tiles<K, RRingOp<K, SAMPLED>, KMC_RSCAT_PF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+        stream_tiles<K, RRingOp<K, SAMPLED>, kRScatPF, 0>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
         op.finish(p.cnt + li);
         __syncthreads();
     }
@@ -702,12 +675,12 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
         // left the loop waiting on HBM latency
         uint64_t i = threadIdx.x;
         const auto ld = [&](uint64_t k) { return v[k]; };  // (non-temporal loads: no gain, same-box A/B)
-        for (; i + (KMC_R4_U - 1) * 1024 < nvec; i += KMC_R4_U * 1024) {
-            uint4 x[KMC_R4_U];
+        for (; i + (kR4U - 1) * 1024 < nvec; i += kR4U * 1024) {
+            uint4 x[kR4U];
 #pragma unroll
-            for (int u = 0; u < KMC_R4_U; ++u) x[u] = ld(i + 1024u * u);
+            for (int u = 0; u < kR4U; ++u) x[u] = ld(i + 1024u * u);
 #pragma unroll
-            for (int u = 0; u < KMC_R4_U; ++u) add8(x[u]);
+            for (int u = 0; u < kR4U; ++u) add8(x[u]);
         }
         for (; i < nvec; i += 1024) add8(v[i]);
         const uint64_t t = a + nvec * 8;
@@ -718,7 +691,7 @@ __device__ __forceinline__ void hist_list(const uint16_t *ent, uint64_t beg, uin
 // Sampled mode: a list is the G regions [rb[r], rb[r] + rn[r]) of its workgroups,
 // with gaps between them.  The regions' 16-byte vectors are numbered 0 .. V-1 in
 // order (vpre: exclusive prefix of each region's vector count) and thread t takes
-// vectors t, t + 1024, ..., KMC_R4_U in flight, walking its region cursor forward;
+// vectors t, t + 1024, ..., kR4U in flight, walking its region cursor forward;
 // a vector's entries outside its region are skipped.
 constexpr int kMaxRegions = 256;  // workgroups of R1/R3 in sampled mode
 template <int LOW>
@@ -739,11 +712,11 @@ __device__ __forceinline__ void hist_regions(const uint16_t *ent, const uint32_t
         jl = ve - (((hi & 7u) && ve > jf) ? 1u : 0u);
     };
     enter(0);
-    for (uint32_t j0 = threadIdx.x; j0 < V; j0 += KMC_R4_U * 1024) {
-        uint4 x[KMC_R4_U];
-        uint32_t m[KMC_R4_U];  // valid entries of vector u (bit q: entry q)
+    for (uint32_t j0 = threadIdx.x; j0 < V; j0 += kR4U * 1024) {
+        uint4 x[kR4U];
+        uint32_t m[kR4U];  // valid entries of vector u (bit q: entry q)
 #pragma unroll
-        for (int u = 0; u < KMC_R4_U; ++u) {
+        for (int u = 0; u < kR4U; ++u) {
             const uint32_t j = j0 + 1024u * u;
             m[u] = 0u;
             if (j < V) {
@@ -765,7 +738,7 @@ __device__ __forceinline__ void hist_regions(const uint16_t *ent, const uint32_t
             }
         }
 #pragma unroll
-        for (int u = 0; u < KMC_R4_U; ++u) {
+        for (int u = 0; u < kR4U; ++u) {
             const uint32_t e[8] = {x[u].x & 0xFFFFu, x[u].x >> 16, x[u].y & 0xFFFFu, x[u].y >> 16,
                                    x[u].z & 0xFFFFu, x[u].z >> 16, x[u].w & 0xFFFFu, x[u].w >> 16};
             if (m[u] == 0xFFu) {
@@ -845,7 +818,7 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
         }
     };
     fetch(blockIdx.x);
-    bool dirty = true;  // (KMC_R4_FUSE: the list-end pass leaves the bins cleared)
+    bool dirty = true;  // (the list-end pass leaves the bins cleared, but for a recount)
     for (int64_t list = blockIdx.x; list < nlists; list += gridDim.x) {  // list = s*nbk + b
         const int64_t s = list / p.nbk, b = list % p.nbk;
         if (b == 0 && threadIdx.x == 0 && p.status) {  // int32 bins of >= 2^31 windows could wrap
@@ -856,7 +829,7 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
                 __hip_atomic_store(p.status, (uint32_t)KMC_ERR_RECORD_TOO_LONG, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        if (!KMC_R4_FUSE || dirty)
+        if (dirty)
             for (int i = threadIdx.x; i < kWords; i += 1024) h[i] = 0u;
         if (threadIdx.x == 0) s_sum = 0ull;
         uint64_t beg, end;  // entries of the list (REG: beg = 0, end = their number)
@@ -893,8 +866,10 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
         }
         __syncthreads();
         uint32_t *dst = p.stage + s * nbins + b * kBucketBins;
-        if constexpr (KMC_R4_FUSE) {
-            // one pass: stage row written, bins summed (LOW = 16: wrap check) and cleared
+        {
+            // one pass (round 4, same box: R4 4.34 -> 4.19 ms against a sum pass, a
+            // write pass and a clear pass): stage row written, bins summed (LOW = 16:
+            // wrap check) and cleared
             uint32_t part = 0u;
             for (int i = threadIdx.x; i < kWords; i += 1024) {
                 const uint32_t w = h[i];
@@ -915,22 +890,6 @@ __global__ __launch_bounds__(1024) void radix_hist_kernel(RParams p, int64_t nbi
                     else hist_recount<LOW>(p.ent, beg, end, h, dst);
                     dirty = true;
                 }
-            }
-        } else if constexpr (LOW <= 15) {
-            for (int i = threadIdx.x; i < kBucketBins; i += 1024) dst[i] = h[i];
-        } else {
-            uint32_t part = 0u;
-            for (int i = threadIdx.x; i < kWords; i += 1024) part += (h[i] & 0xFFFFu) + (h[i] >> 16);
-            atomicAdd(&s_sum, (unsigned long long)part);
-            __syncthreads();
-            if (s_sum == end - beg) {
-                for (int i = threadIdx.x; i < kWords; i += 1024) {
-                    const uint32_t w = h[i];
-                    reinterpret_cast<uint2 *>(dst)[i] = make_uint2(w & 0xFFFFu, w >> 16);
-                }
-            } else {  // a bin wrapped: exact recount, half of the bins at a time
-                if constexpr (REG) hist_recount_regions<LOW>(p.ent, s_rb, s_rn, nreg, h, dst);
-                else hist_recount<LOW>(p.ent, beg, end, h, dst);
             }
         }
         __syncthreads();  // h and s_sum are reused by the next list
