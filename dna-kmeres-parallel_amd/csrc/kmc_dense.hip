@@ -72,8 +72,6 @@ struct Params {
     uint32_t spill_cap;
     uint32_t *status;        // the call's status word (kmc_dense_args::status, or the device's host-mapped
                              // kmc_dense_status flag): a kmc_status code when the counts are not valid
-    int slab8;               // k = 8: slab slots hold one byte per bin (bin order), counts >= 256 as
-                             // spill entries (chosen when a workgroup's windows per bin are few)
 };
 
 // Store a kmc_status code in the call's status word (a plain system-scope store:
@@ -398,41 +396,6 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 // LDS: the halves are exact, wraps live in spills); the LDS cleared
                 const auto flush = [&]() {
                     uint32_t dsum = 0u;
-                    if (!entire && p.slab8) {
-                        // the slab in bytes, bin order (bin c at byte c: word i's halves
-                        // at bytes i and i + NW): 16 words per lane and round, two
-                        // 16-byte stores; a half >= 256 keeps its low byte here and the
-                        // rest as a spill entry (windows / 256 of them at most)
-                        uint8_t *d8 = reinterpret_cast<uint8_t *>(dst);
-                        for (int i = tid; i < NW / 16; i += BLOCK) {
-                            uint4 *h4 = reinterpret_cast<uint4 *>(h) + 4 * i;
-                            uint32_t lo8[4], hi8[4];
-#pragma unroll
-                            for (int q = 0; q < 4; ++q) {
-                                const uint4 v = h4[q];
-                                h4[q] = make_uint4(0u, 0u, 0u, 0u);
-                                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-                                uint32_t l = 0u, u = 0u;
-#pragma unroll
-                                for (int e = 0; e < 4; ++e) {
-                                    dsum += (x[e] & 0xFFFFu) + (x[e] >> 16);
-                                    if (__builtin_expect((x[e] & 0xFF00FF00u) != 0u, 0)) {
-                                        const uint32_t word = (uint32_t)(16 * i + 4 * q + e);
-                                        if (x[e] & 0xFF00u) p16_spill(pc, (int32_t)word, (int32_t)(x[e] & 0xFF00u));
-                                        if (x[e] & 0xFF000000u)
-                                            p16_spill(pc, (int32_t)(word | 0x8000u), (int32_t)((x[e] >> 16) & 0xFF00u));
-                                    }
-                                    l |= (x[e] & 0xFFu) << (8 * e);
-                                    u |= ((x[e] >> 16) & 0xFFu) << (8 * e);
-                                }
-                                lo8[q] = l;
-                                hi8[q] = u;
-                            }
-                            reinterpret_cast<uint4 *>(d8)[i] = make_uint4(lo8[0], lo8[1], lo8[2], lo8[3]);
-                            reinterpret_cast<uint4 *>(d8 + NW)[i] = make_uint4(hi8[0], hi8[1], hi8[2], hi8[3]);
-                        }
-                        return dsum;
-                    }
                     if (!entire) {  // the slab: 16 bytes per lane
                         for (int i = tid; i < NW / 4; i += BLOCK) {
                             const uint4 v = reinterpret_cast<const uint4 *>(h)[i];
@@ -533,10 +496,7 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
     constexpr int RR = 256 / RC;                   // rows over the slots
     constexpr int RW = 4 * RC;                     // words per block
     constexpr int NH = P16 ? 2 : 1;                // counters per word
-    // byte slab (k = 8, p.slab8): the block's bins are 2 x 64 bytes per slot, read
-    // as 8 columns of 16 bytes x 32 rows
-    constexpr int RR8 = P16 ? 256 / (2 * RW / 16) : RR;
-    __shared__ uint32_t s_part[RR8 > RR ? RR8 : RR][RW * NH];
+    __shared__ uint32_t s_part[RR][RW * NH];
     __shared__ uint32_t s_out[RW * NH];
     const int tid = threadIdx.x, col = tid % RC, row = tid / RC;
     const int64_t c0 = (int64_t)blockIdx.x * RW;
@@ -594,59 +554,32 @@ __global__ __launch_bounds__(256) void reduce_dense_kernel(Params p) {
                 });
             continue;
         }
+        uint32_t acc[4 * NH] = {};
         // slot of workgroup wf + i: 2 (wf + i) for i > 0; wf's first or second
         const int64_t sf = 2 * wf + (p.slot_rec[2 * wf] == s ? 0 : 1);
         const int64_t n = wlast - wf + 1;
-        // the slots' sums per row of s_part
-        const auto sum_words = [&]() {
-            uint32_t acc[4 * NH] = {};
 #pragma unroll 4
-            for (int64_t i = row; i < n; i += RR) {
-                const int64_t slot = i == 0 ? sf : 2 * (wf + i);
-                const uint4 v = reinterpret_cast<const uint4 *>(p.slab + slot * NB + c0)[col];
-                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+        for (int64_t i = row; i < n; i += RR) {
+            const int64_t slot = i == 0 ? sf : 2 * (wf + i);
+            const uint4 v = reinterpret_cast<const uint4 *>(p.slab + slot * NB + c0)[col];
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if constexpr (P16) {
-                        acc[e] += x[e] & 0xFFFFu;  // bin c
-                        acc[4 + e] += x[e] >> 16;  // bin c + NW
-                    } else {
-                        acc[e] += x[e];
-                    }
+            for (int e = 0; e < 4; ++e) {
+                if constexpr (P16) {
+                    acc[e] += x[e] & 0xFFFFu;  // bin c
+                    acc[4 + e] += x[e] >> 16;  // bin c + NW
+                } else {
+                    acc[e] += x[e];
                 }
             }
-#pragma unroll
-            for (int e = 0; e < 4 * NH; ++e) s_part[row][(e / 4) * RW + col * 4 + e % 4] = acc[e];
-        };
-        int rows = RR;
-        if constexpr (P16) {
-            if (p.slab8) {  // byte slots: bins [c0, c0 + RW) and [NW + c0, ...) in 8 columns
-                constexpr int C8 = 2 * RW / 16;
-                const int c8 = tid % C8, r8 = tid / C8, hf = c8 / (C8 / 2), b8 = 16 * (c8 % (C8 / 2));
-                uint32_t a8[16] = {};
-#pragma unroll 4
-                for (int64_t i = r8; i < n; i += RR8) {
-                    const int64_t slot = i == 0 ? sf : 2 * (wf + i);
-                    const uint8_t *d8 = reinterpret_cast<const uint8_t *>(p.slab + slot * NB);
-                    const uint4 v = *reinterpret_cast<const uint4 *>(d8 + hf * NW + c0 + b8);
-                    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) a8[e] += (x[e / 4] >> (8 * (e % 4))) & 0xFFu;
-                }
-#pragma unroll
-                for (int e = 0; e < 16; ++e) s_part[r8][hf * RW + b8 + e] = a8[e];
-                rows = RR8;
-            } else {
-                sum_words();
-            }
-        } else {
-            sum_words();
         }
+#pragma unroll
+        for (int e = 0; e < 4 * NH; ++e) s_part[row][(e / 4) * RW + col * 4 + e % 4] = acc[e];
         __syncthreads();
         for (int i = tid; i < RW * NH; i += 256) {
             uint32_t t = 0u;
 #pragma unroll 8
-            for (int r = 0; r < rows; ++r) t += s_part[r][i];
+            for (int r = 0; r < RR; ++r) t += s_part[r][i];
             s_out[i] = t;
         }
         if (spills) {
@@ -728,10 +661,8 @@ void *kernel_ptr() {
 thread_local int t_reserved_cus = 0;
 
 #ifdef KMC_DIAG_HOOKS
-// test hooks (diagnostic library only): spill list capacity per workgroup (0: the
-// bound); the k = 8 slab format (-1: by the windows per workgroup, 0: 16-bit, 1: bytes)
+// test hook (diagnostic library only): spill list capacity per workgroup (0: the bound)
 std::atomic<uint32_t> g_diag_spill_cap{0};
-std::atomic<int> g_diag_slab8{-1};
 #endif
 
 template <int K, class Idx>
@@ -829,23 +760,14 @@ inline WsLayout ws_layout(int k, int G, uint32_t spill_cap) {
 // windows * (1/32768 + 3/65536) = windows * 5/65536 <= windows / 4096 entries.
 constexpr uint32_t kSpillWindowsPerEntry = 4096;
 static_assert(5u * kSpillWindowsPerEntry <= 65536u, "HM 3 scan + HM 1 recount entries exceed the spill cap");
-// The byte slab adds an entry per half >= 256 at a partial piece's flush, and a
-// piece recounted after a wrap flushes twice: at most 2 * windows / 256 more.
-inline uint32_t spill_cap_for(int64_t tiles_per_wg, bool slab8) {
+inline uint32_t spill_cap_for(int64_t tiles_per_wg) {
     const int64_t windows = tiles_per_wg * kTile;
-    return (uint32_t)(windows / kSpillWindowsPerEntry + (slab8 ? windows / 128 : 0) + 64);
+    return (uint32_t)(windows / kSpillWindowsPerEntry + 64);
 }
-
-// k = 8 partial pieces flushed as bytes when a workgroup counts at most
-// kSlab8Tiles * 1024 windows (<= 128 per bin on average, so a byte rarely
-// overflows): an 8-way shard of the bench's 10 Gbase job (4 768 tiles per
-// workgroup) writes and reduces 16 MB of slab instead of 32.
-constexpr int64_t kSlab8Tiles = 8192;
 
 struct Plan {
     int G;
     uint32_t spill_cap;
-    bool slab8;
     WsLayout L;
 };
 
@@ -855,18 +777,12 @@ int make_plan(int device, bool derive, int64_t wl, int64_t wh, Plan &pl) {
     int e = grid_size<K, Idx>(device, G);
     if (e) return e;
     pl.spill_cap = 0;
-    pl.slab8 = false;
     if (!derive) {
         const int64_t tiles = wh > wl ? ((wh + kTile - 1) >> kTileShift) - (wl >> kTileShift) : 0;
         if (tiles < G) G = tiles > 0 ? (int)tiles : 1;
         const int64_t tpw = tiles > 0 ? (tiles + G - 1) / G : 1;
         if (Cfg<K>::P16) {
-            pl.slab8 = tpw <= kSlab8Tiles;
-#ifdef KMC_DIAG_HOOKS
-            const int d8 = g_diag_slab8.load();
-            if (d8 >= 0) pl.slab8 = d8 != 0;
-#endif
-            pl.spill_cap = spill_cap_for(tpw, pl.slab8);
+            pl.spill_cap = spill_cap_for(tpw);
 #ifdef KMC_DIAG_HOOKS
             const uint32_t dc = g_diag_spill_cap.load();
             if (dc) pl.spill_cap = dc;
@@ -968,7 +884,6 @@ int run_dense(const Request &q, hipStream_t st) {
     p.slab = reinterpret_cast<uint32_t *>(base + pl.L.slab);
     p.spill = Cfg<K>::P16 ? reinterpret_cast<Spill *>(base + pl.L.spill) : nullptr;
     p.spill_cap = pl.spill_cap;
-    p.slab8 = pl.slab8 ? 1 : 0;
     p.status = q.status;
     if (!p.status) {
         uint32_t *sh = nullptr;
@@ -1064,14 +979,6 @@ extern "C" int kmc_dense_status(int device) { return take_status(device); }
 // capacity per workgroup, lowered so that an overflow raises the status flag.
 extern "C" KMC_DIAG_API int kmc_diag_dense_spill_cap(unsigned cap) {
     g_diag_spill_cap.store(cap);
-    return KMC_OK;
-}
-
-// Test hook (diagnostic library only): the k = 8 slab format, -1 chosen by the
-// windows per workgroup (the product's rule), 0 16-bit slots, 1 byte slots.
-extern "C" KMC_DIAG_API int kmc_diag_dense_slab8(int mode) {
-    if (mode < -1 || mode > 1) return KMC_ERR_INVALID_ARG;
-    g_diag_slab8.store(mode);
     return KMC_OK;
 }
 #endif

@@ -73,8 +73,7 @@ class diag:
     """Context manager: inside it every binding calls lib/libkmc_diag.so, the same
     library built with the test hooks (kmc_diag_radix_mode, kmc_diag_canon_claim_cap,
     kmc_diag_canon_sort_cap, kmc_diag_dense_spill_cap) that force an algorithm
-    choice (kmc_diag_canon_sort_cap_big, kmc_diag_canon_direct, kmc_diag_dense_slab8
-    too); libkmc.so
+    choice (kmc_diag_canon_sort_cap_big, kmc_diag_canon_direct too); libkmc.so
     exports none of them.  `with kmc.diag() as D: D.kmc_diag_...`"""
 
     def __enter__(self):
@@ -90,7 +89,6 @@ class diag:
             _diag_lib.kmc_diag_canon_fallback_detail.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_uint,
                                                                  ctypes.POINTER(ctypes.c_ulonglong)]
             _diag_lib.kmc_diag_dense_spill_cap.argtypes = [ctypes.c_uint]
-            _diag_lib.kmc_diag_dense_slab8.argtypes = [ctypes.c_int]
         self._prev = _active
         _active = _diag_lib
         return _diag_lib
@@ -104,7 +102,6 @@ class diag:
         L.kmc_diag_canon_sort_cap(1 << 30)  # (also restores the big instance's cap)
         L.kmc_diag_canon_direct(1)
         L.kmc_diag_dense_spill_cap(0)
-        L.kmc_diag_dense_slab8(-1)
         _active = self._prev
         return False
 

@@ -8,7 +8,6 @@
 #          profile        scripts/profile_bench.sh: kernel trace + HBM and LDS PMC passes
 #          cbench[:CFGS]  scripts/cbench.py --configs CFGS (default c1,c3,c4,c4r) under the kernel trace
 #          shard          scripts/shardbench.py (one rank's step of an N-way job, N = 1, 2, 4, 8)
-#          shardab        the same at N = 1, 4, 8, 16-bit against byte slab slots, two passes
 #          fuzz           the dense and canonical fuzzers
 # Every step has its own time limit; the first failing step ends the call.
 # Output: gpurun_out/TAG/<step>.log (+ rocprofv3 directories).
@@ -35,7 +34,6 @@ for s in "$@"; do
         cbench:*) run 900 $O/cbench.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/cbench_prof -o cb \
                       -- python3 scripts/cbench.py --iters 3 --configs "${s#cbench:}" ;;
         shard) run 600 $O/shard.log python scripts/shardbench.py ;;
-        shardab) run 600 $O/shardab.log python scripts/shardbench.py --worlds 1,4,8 --slab8 ab --passes 2 ;;
         fuzz) run 600 $O/fuzz_dense.log python scripts/fuzz_dense.py && run 600 $O/fuzz_canonical.log python scripts/fuzz_canonical.py ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

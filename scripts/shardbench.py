@@ -5,10 +5,7 @@ all-reduce: what each rank's step costs when the 10 Gbase job is cut N ways
 time (the whole kmc_count_dense_ex call: histogram kernel + slab reduce + spill
 fix-up, back to back), the histogram kernel's time (HIP events around it) and
 the step overhead; the worst rank bounds the N-GPU step.
---slab8 0|1|ab: the k = 8 slab format forced through the diagnostic library
-(16-bit / byte slots; ab: both, alternating, same process); default: the
-library's own choice (bytes at <= 8 192 tiles per workgroup).
-Usage: python scripts/shardbench.py [--worlds 1,2,4,8] [--steps 20] [--ranks all|first] [--slab8 ab]"""
+Usage: python scripts/shardbench.py [--worlds 1,2,4,8] [--steps 20] [--ranks all|first]"""
 import argparse
 import json
 import os
@@ -28,8 +25,6 @@ def main():
     ap.add_argument("--records", type=int, default=10)
     ap.add_argument("--record-len", type=int, default=1_000_000_000)
     ap.add_argument("--ranks", default="first", help="first: rank 0 and the last rank; all: every rank")
-    ap.add_argument("--slab8", default="", help="0, 1 or ab (diagnostic library); default: the product choice")
-    ap.add_argument("--passes", type=int, default=1)
     a = ap.parse_args()
     import torch
 
@@ -40,14 +35,8 @@ def main():
     k, L = a.k, a.record_len
     seed = bench.SEED_BASE + k
     nb = 1 << (2 * k)
-    modes = {"": [None], "0": [0], "1": [1], "ab": [0, 1]}[a.slab8]
-    jobs = [(w, m) for _ in range(a.passes) for w in [int(x) for x in a.worlds.split(",")] for m in modes]
-    for world, mode in jobs:
+    for world in [int(x) for x in a.worlds.split(",")]:
         ranks = range(world) if a.ranks == "all" else sorted({0, world - 1})
-        if mode is not None:
-            dg = kmc.diag()
-            D = dg.__enter__()
-            assert D.kmc_diag_dense_slab8(mode) == 0
         for rank in ranks:
             plan = bench.rank_plan("strong", world, rank, a.records, L, k)
             base, hold_hi = plan["hold"]
@@ -85,15 +74,12 @@ def main():
             kmc.trace_events(None, None)
             kern = sorted(b.elapsed_time(e) for b, e in ev)
             kern_ms = kern[len(kern) // 2]
-            print(json.dumps({"world": world, "rank": rank, "slab8": mode, "win_bytes": win_hi - win_lo,
-                              "windows_counted": tot,
+            print(json.dumps({"world": world, "rank": rank, "win_bytes": win_hi - win_lo, "windows_counted": tot,
                               "step_ms": round(step_ms, 4), "kernel_ms": round(kern_ms, 4),
                               "overhead_us": round((step_ms - kern_ms) * 1e3, 1),
                               "GBps_kernel": round((win_hi - win_lo) / kern_ms / 1e6, 1)}), flush=True)
             del data, out, ws
             torch.cuda.empty_cache()
-        if mode is not None:
-            dg.__exit__(None, None, None)
 
 
 if __name__ == "__main__":

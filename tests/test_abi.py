@@ -39,7 +39,7 @@ def test_diag_library_adds_only_the_test_hooks(kmc):
     assert hooks == ["kmc_diag_canon_claim_cap", "kmc_diag_canon_direct", "kmc_diag_canon_fallback",
                      "kmc_diag_canon_fallback_detail",
                      "kmc_diag_canon_sort_cap",
-                     "kmc_diag_canon_sort_cap_big", "kmc_diag_dense_slab8", "kmc_diag_dense_spill_cap", "kmc_diag_radix_mode"]
+                     "kmc_diag_canon_sort_cap_big", "kmc_diag_dense_spill_cap", "kmc_diag_radix_mode"]
     assert sorted(set(got) - set(hooks)) == kmc.header_symbols()
     assert kmc.lib() is not None
     with kmc.diag() as D:  # inside diag() every binding uses the diagnostic library

@@ -607,48 +607,6 @@ def test_dense_spill_overflow_raises_status(kmc, oracle, cuda):
     np.testing.assert_array_equal(inv.cpu().numpy(), exp_inv)
 
 
-@pytest.mark.parametrize("slab8", [0, 1])
-def test_dense_byte_slab_vs_oracle(kmc, oracle, cuda, slab8):
-    """k = 8 partial pieces in byte slab slots (chosen for shards of <= 8 192 tiles
-    per workgroup, forced here through the diagnostic library) against 16-bit ones:
-    bit-exact with the oracle on inputs whose per-workgroup bins pass 255 -- tandem
-    repeats (a 2-base unit puts 512 windows per tile on two bins), poly-A runs of a
-    few tiles, and a 64 MB poly-A record whose 16-bit halves wrap, so that its pieces
-    are recounted and flushed twice (the first flush's byte-overflow entries
-    superseded) -- and on random records cut into many pieces."""
-    import torch
-    rng = np.random.default_rng(808 + slab8)
-    acgt = np.frombuffer(b"ACGT", np.uint8)
-    rnd = lambda n: acgt[rng.integers(0, 4, n)]
-    tandem = np.frombuffer(b"AC" * 40_000, np.uint8)
-    mixed = np.concatenate([rnd(30_000), tandem, np.full(5_000, ord("A"), np.uint8), rnd(20_000),
-                            np.frombuffer(b"GATTACA" * 3_000, np.uint8), rnd(7_777)])
-    cases = [random_records(rng, [300_000, 12_345, 99_999, 1], 0.002, 0.002),
-             (np.concatenate([np.append(mixed, np.uint8(0)), np.append(rnd(50_000), np.uint8(0))]),
-              np.array([0, mixed.size + 1, mixed.size + 50_002], np.int64)),
-             (np.concatenate([np.append(np.full(64 << 20, ord("A"), np.uint8), np.uint8(0)),
-                              np.append(tandem, np.uint8(0))]),
-              np.array([0, (64 << 20) + 1, (64 << 20) + tandem.size + 2], np.int64))]
-    dv = torch.cuda.current_device()
-    with kmc.diag() as D:
-        assert D.kmc_diag_dense_slab8(slab8) == 0
-        for data, idx in cases:
-            exp, exp_inv = oracle.count_dense(data, idx, 8)
-            got, inv = run_dense(kmc, cuda, data, idx, 8)
-            assert D.kmc_dense_status(dv) == 0
-            np.testing.assert_array_equal(got, exp)
-            np.testing.assert_array_equal(inv, exp_inv)
-            # a window range of the same buffer (a shard: record pieces at both ends)
-            lo, hi = data.size // 3 + 5, 2 * data.size // 3 + 11
-            d, di = dev(data, cuda), dev(idx, cuda)
-            out = torch.empty((1 << 16, idx.size - 1), dtype=torch.int32, device=cuda)
-            st = torch.zeros(1, dtype=torch.int32, device=cuda)
-            kmc.count_dense_ex(kmc.dense_args(d, di, 8, out.view(-1), read=(lo, min(hi + 7, data.size)),
-                                              win=(lo, hi), status=st))
-            kmc.dense_status_check(st)
-            np.testing.assert_array_equal(out.cpu().numpy(), oracle.count_dense(data, idx, 8, win=(lo, hi))[0])
-
-
 @pytest.mark.parametrize("k", [4, 8, 13])
 def test_dense_record_of_2p31_windows_reports_error(kmc, cuda, k):
     """int32 counts (the reference's, main.cu:598,637) could wrap for a record of
