@@ -44,6 +44,9 @@ namespace kmc {
 // k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
 // spill entries (section 4.1 of DESIGN.md: 64 / 256 / 512 / 1 024 measured)
 constexpr int kHm3Scan = 256;
+// Tiles per chunk of the workgroup's shared tile counter (stream_chunks, round 5),
+// and chunks per workgroup between two scans (256 tiles per wave, as before).
+constexpr int kChunk = 16;
 thread_local hipEvent_t t_trace_before = nullptr;
 thread_local hipEvent_t t_trace_after = nullptr;
 namespace {
@@ -248,19 +251,18 @@ struct DenseOp {
         count_tile<K, R, HM, MASKED>(lo, hi, W, h, lane);
         if constexpr (HM == 3) nwin += MASKED ? (uint32_t)__builtin_popcount(W) : 16u;
     }
-    __device__ __forceinline__ void after_iter(int64_t i, int64_t per, bool) {
+    // HM 3: hot halves (>= 32768) go to spill entries every kHm3Scan tiles per
+    // wave (stream_chunks' segments), so a half wraps only if one k-mer takes
+    // >= 32768 of the workgroup's NWAVES * kHm3Scan * 1024 windows in between (long
+    // low-complexity runs); wraps stay detected by the piece total
+    __device__ __forceinline__ void segment_end() {
         if constexpr (HM == 3) {
-            // hot halves (>= 32768) go to spill entries every kHm3Scan tiles per
-            // wave, so a half wraps only if one k-mer takes >= 32768 of the
-            // workgroup's NWAVES * kHm3Scan * 1024 windows in between (long
-            // low-complexity runs); wraps stay detected by the piece total
-            if ((i % kHm3Scan) == kHm3Scan - 1 && i + 1 < per) {
-                lds_barrier();
-                p16_scan<BLOCK, 32768u>(pc);
-                lds_barrier();
-            }
+            lds_barrier();
+            p16_scan<BLOCK, 32768u>(pc);
+            lds_barrier();
         }
     }
+    static constexpr int kSegChunks = HM == 3 ? BLOCK / 64 * kHm3Scan / kChunk : 0;
 };
 
 // HM 3's exact recount of the windows [ps, pe) of a piece whose 16-bit halves
@@ -326,6 +328,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 misc[3] = 0u;
                 misc[4] = 0u;
                 misc[5] = 0u;
+                misc[7] = 0u;
             }
             const bool le = tid < p.n && rec_off<Idx>(p, tid) <= R0;
             for (int i = tid; i < NW / 4; i += BLOCK) reinterpret_cast<uint4 *>(h)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -346,6 +349,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                 misc[3] = 0u;
                 misc[4] = 0u;
                 misc[5] = 0u;
+                misc[7] = 0u;
                 misc[1] = (uint32_t)lo;
                 misc[2] = (uint32_t)((uint64_t)lo >> 32);
             }
@@ -370,14 +374,13 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             const int64_t pe = ce < R1 ? ce : R1;
             if (ps >= pe) continue;
             pc.rec = s;
-            // this piece's tiles, split into contiguous per-wave runs
+            // this piece's tiles, in chunks taken by the waves as they go (misc[7]:
+            // the chunk counter, zero at the piece's start)
             const int64_t tp0 = ps >> kTileShift;
             const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
-            const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
-            const int64_t a0 = tp0 + (int64_t)wave * per;
-            const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
-            DenseOp<K, R, HM, BLOCK> op(h, lane, pc);
-            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+            using Op = DenseOp<K, R, HM, BLOCK>;
+            Op op(h, lane, pc);
+            stream_chunks<K, kChunk, Op::kSegChunks>(p.data, tp0, tp1, ps, pe, g.rl, g.rh, lane, &misc[7], op);
             if constexpr (HM == 3) {
                 const uint32_t wsum = wave_sum(op.nwin);
                 if (lane == 0) atomicAdd(&misc[3], wsum);
@@ -460,6 +463,7 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
                     else dst[c] = v;
                 }
             }
+            if (tid == 0) misc[7] = 0u;  // (every wave's last take of this piece is behind the barrier after it)
             __syncthreads();
             ++npieces;
         }

@@ -384,6 +384,160 @@ __device__ __forceinline__ void stream_tiles(const char *__restrict__ data, int6
     for (int64_t i = n; i < per; ++i) op.after_iter(i, per, false);
 }
 
+// ---------------------------------------------------------------------------
+// Chunked streaming (round 5, the dense histogram): the tiles of a piece are
+// handed to the workgroup's waves in chunks of C tiles from an LDS counter instead
+// of one contiguous run per wave.  Waves of one workgroup do not run at one speed
+// on the LDS-bound k = 8 histogram: between two hot-half scans (256 tiles per wave)
+// the fastest took 131 us and the slowest 239 us, and every scan barrier waits for
+// the slowest (scripts/dense_phase_prof.py, profiles/r05m_dense_phase_prof.txt).
+// Each wave takes its next chunk when it starts the current one, so the prefetch
+// ring runs on into it without a break; the halo of a chunk's last tile (lane 0 of
+// the physically next tile, which belongs to another chunk) is loaded by lane 0
+// alone at the chunk's start.  SEGC > 0: after every SEGC chunks of the piece the
+// waves meet for op.segment_end() (the k = 8 scans), each wave once per segment
+// boundary whether or not it took a chunk in between.
+template <int K, int C, int PF = kStreamPF, int NT = kStreamNT>
+struct ChunkStream {
+    static constexpr int NS = PF + 1;
+    static_assert(C % NS == 0 && C > PF, "a chunk is whole turns of the prefetch ring");
+    const char *__restrict__ data;
+    int64_t ps, pe, rl, rh, tend;
+    int lane;
+    __amdgpu_buffer_rsrc_t rsrc;
+    int64_t base_off;
+    int64_t cb, nb;  // the current chunk's first tile; the next one's (-1: none)
+    uint4 r[NS];
+    uint4 hz;        // lane 0: the 16 bytes at tile cb + C (the halo of the chunk's last tile)
+    uint32_t c_cur, v_cur;
+
+    // tile t of this lane, or zeros (no memory access) when !valid
+    __device__ __forceinline__ uint4 load_sel(int64_t t, bool valid) const {
+        const int64_t off = (t << kTileShift) - base_off + (int64_t)lane * 16;
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, valid ? (int)(uint32_t)off : -16, 0, NT ? 2 : 0);
+        return make_uint4(x[0], x[1], x[2], x[3]);
+    }
+
+    // a new current chunk: resource based at it, the halo of its last tile
+    __device__ __forceinline__ void begin_chunk() {
+        base_off = tile_base(cb, rl);
+        rsrc = tile_rsrc(data, base_off, rh);
+        const int64_t th = cb + C;
+        hz = load_sel(th, lane == 0);
+        if (tile_straddles(th, rl, rh)) hz = mask_range(hz, th << kTileShift, rl, rh);
+    }
+
+    // position j (j % NS == S) of the current chunk
+    template <int S, class Op>
+    __device__ __forceinline__ void step(int j, Op &op) {
+        const int64_t t = cb + j;
+        constexpr int SN = (S + 1) % NS, SL = (S + PF) % NS;
+        const int jl = j + PF;  // the tile PF positions ahead: this chunk's, or the next one's
+        r[SL] = jl < C ? load_sel(cb + jl, true) : load_sel(nb + (jl - C), nb >= 0);
+        const int64_t tn = j + 1 < C ? t + 1 : nb;  // the tile after t in this wave's sequence
+        if (tn >= 0 && tile_straddles(tn, rl, rh))
+            r[SN] = mask_range(r[SN], (tn << kTileShift) + (int64_t)lane * 16, rl, rh);
+        const uint4 r_cur = r[S], r_nxt = r[SN];
+        uint32_t c_nxt, v_nxt;
+        decode16(r_nxt, c_nxt, v_nxt);
+        // halo: next lane's 16 bases; lane 63 takes lane 0 of tile t + 1 -- the next
+        // in the sequence, except after the chunk's last tile
+        const bool edge = S == NS - 1 && j == C - 1;  // (wave-uniform)
+        uint32_t c_h = c_nxt, v_h = v_nxt;
+        if (edge) decode16(hz, c_h, v_h);
+        uint32_t hc = from_next_lane(c_cur);
+        uint32_t hv = from_next_lane(v_cur);
+        const uint32_t c0 = __builtin_amdgcn_readlane(c_h, 0);
+        const uint32_t v0 = __builtin_amdgcn_readlane(v_h, 0);
+        if (lane == 63) {
+            hc = c0;
+            hv = v0;
+        }
+        op.before_tile();
+        const int64_t base = t << kTileShift;
+        const bool interior = base >= ps && base + kTile <= pe;  // wave-uniform
+        if (interior && !__any((v_cur | hv) != 0u)) {
+            op.template tile<false>(c_cur, hc, 0xFFFFu);
+        } else {
+            const int64_t pos = base + (int64_t)lane * 16;
+            const int64_t dlo = ps - pos, dhi = pe - pos;
+            const uint32_t mhi = dhi >= 16 ? 0xFFFFu : (dhi <= 0 ? 0u : ((1u << (uint32_t)dhi) - 1u));
+            const uint32_t mlo = dlo <= 0 ? 0xFFFFu : (dlo >= 16 ? 0u : ((0xFFFFu << (uint32_t)dlo) & 0xFFFFu));
+            const uint32_t b_own = bad_mask16(r_cur);
+            uint32_t b_next = from_next_lane(b_own);
+            const uint32_t b0 = __builtin_amdgcn_readlane(bad_mask16(edge ? hz : r_nxt), 0);
+            if (lane == 63) b_next = b0;
+            const uint32_t W = ~smear<K>(b_own | (b_next << 16)) & mhi & mlo & 0xFFFFu;
+            op.template tile<true>(c_cur, hc, W);
+        }
+        c_cur = c_nxt;
+        v_cur = v_nxt;
+    }
+
+    // positions j .. j+NS-1 of the current chunk, stopping at the piece's end
+    template <int S, class Op>
+    __device__ __forceinline__ void steps(int j, Op &op) {
+        if constexpr (S < NS) {
+            if (cb + j + S < tend) {
+                step<S>(j + S, op);
+                steps<S + 1>(j, op);
+            }
+        }
+    }
+};
+
+template <int K, int C, int SEGC, class Op, int PF = kStreamPF, int NT = kStreamNT>
+__device__ __forceinline__ void stream_chunks(const char *__restrict__ data, int64_t tp0, int64_t tp1, int64_t ps,
+                                              int64_t pe, int64_t rl, int64_t rh, int lane, uint32_t *ctr, Op &op) {
+    using CS = ChunkStream<K, C, PF, NT>;
+    const int64_t nch = tp1 > tp0 ? (tp1 - tp0 + C - 1) / C : 0;
+    const auto grab = [&]() -> int64_t {  // the next chunk of the piece, or -1 (wave-uniform)
+        uint32_t c = 0u;
+        if (lane == 0) c = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        c = __builtin_amdgcn_readfirstlane(c);
+        return (int64_t)c < nch ? (int64_t)c : -1;
+    };
+    int64_t seg = 0;  // segment boundaries this wave has passed
+    int64_t c = grab();
+    if (c >= 0) {
+        CS cs;
+        cs.data = data;
+        cs.ps = ps;
+        cs.pe = pe;
+        cs.rl = rl;
+        cs.rh = rh;
+        cs.tend = tp1;
+        cs.lane = lane;
+        cs.cb = tp0 + c * C;
+        cs.nb = -1;
+        cs.begin_chunk();
+#pragma unroll
+        for (int q = 0; q < CS::NS; ++q) cs.r[q] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int q = 0; q < PF; ++q) cs.r[q] = cs.load_sel(cs.cb + q, true);
+        if (tile_straddles(cs.cb, rl, rh))
+            cs.r[0] = mask_range(cs.r[0], (cs.cb << kTileShift) + (int64_t)lane * 16, rl, rh);
+        decode16(cs.r[0], cs.c_cur, cs.v_cur);
+        int64_t nc = grab();
+        for (;;) {
+            cs.nb = nc >= 0 ? tp0 + nc * C : -1;
+            for (int j = 0; j < C; j += CS::NS) cs.template steps<0>(j, op);
+            if (nc < 0) break;
+            if constexpr (SEGC > 0) {
+                for (; seg < nc / SEGC; ++seg) op.segment_end();
+            }
+            cs.cb = cs.nb;
+            cs.begin_chunk();
+            nc = grab();
+        }
+    }
+    if constexpr (SEGC > 0) {
+        const int64_t nseg = (nch + SEGC - 1) / SEGC;
+        for (; seg < nseg - 1; ++seg) op.segment_end();
+    }
+}
+
 // Code of window j (bases j .. j+K-1, K <= 16) of a lane with bases lo : hi.
 template <int K>
 __device__ __forceinline__ uint32_t window_code_rt(uint32_t lo, uint32_t hi, int j) {
