@@ -44,8 +44,12 @@ namespace kmc {
 // k == 8, HM 3: tiles per wave between two scans that move hot 16-bit halves to
 // spill entries (section 4.1 of DESIGN.md: 64 / 256 / 512 / 1 024 measured)
 constexpr int kHm3Scan = 256;
-// Tiles per chunk of the workgroup's shared tile counter (stream_chunks, round 5),
-// and chunks per workgroup between two scans (256 tiles per wave, as before).
+// k >= 7: tiles per chunk of the workgroup's shared tile counter (stream_chunks,
+// round 5).  Same box, kernel alone over 10 Gbase (profiles/r05o_chunk_ab.txt):
+// k = 8 2.242 ms with one contiguous run per wave, 2.15 / 2.07-2.09 / 2.05-2.07 /
+// 2.05-2.08 ms with chunks of 4 / 8 / 16 / 32 tiles; k = 7 2.14 -> 2.06 (16); k <= 6
+// (HBM-bound, the more VGPRs of the chunked loop cost one wave per SIMD) keep the
+// contiguous runs: k = 4 1.77-1.79 against 1.84-1.92 ms chunked.
 constexpr int kChunk = 16;
 thread_local hipEvent_t t_trace_before = nullptr;
 thread_local hipEvent_t t_trace_after = nullptr;
@@ -263,6 +267,7 @@ struct DenseOp {
         }
     }
     static constexpr int kSegChunks = HM == 3 ? BLOCK / 64 * kHm3Scan / kChunk : 0;
+    __device__ __forceinline__ void after_iter(int64_t, int64_t, bool) {}  // (k <= 6: stream_tiles)
 };
 
 // HM 3's exact recount of the windows [ps, pe) of a piece whose 16-bit halves
@@ -298,7 +303,6 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     constexpr bool P16 = HM != 0;
     constexpr int NB = 1 << (2 * K);
     constexpr int NW = P16 ? NB / 2 : NB * R;
-    constexpr int NWAVES = BLOCK / 64;
     // static LDS: the histogram's address is a link-time constant, folded into the
     // ds_add offset (dynamic LDS costs one v_add per window)
     __shared__ __attribute__((aligned(16))) uint32_t smem[NW + 8];
@@ -306,7 +310,6 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
     uint32_t *misc = smem + NW;  // [0] spill count, [1],[2] first record, [3] windows added, [4] decoded sum
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar tile bookkeeping
     const int w = blockIdx.x;
     const Geom g = make_geom<Idx>(p);
     const int64_t tb = g.T0 + (int64_t)w * g.tpw;
@@ -374,13 +377,23 @@ __global__ __launch_bounds__(BLOCK) void count_dense_kernel(Params p) {
             const int64_t pe = ce < R1 ? ce : R1;
             if (ps >= pe) continue;
             pc.rec = s;
-            // this piece's tiles, in chunks taken by the waves as they go (misc[7]:
-            // the chunk counter, zero at the piece's start)
+            // this piece's tiles: k >= 7 in chunks taken by the waves as they go
+            // (misc[7]: the chunk counter, zero at the piece's start), k <= 6 in one
+            // contiguous run per wave
             const int64_t tp0 = ps >> kTileShift;
             const int64_t tp1 = ((pe - 1) >> kTileShift) + 1;
             using Op = DenseOp<K, R, HM, BLOCK>;
             Op op(h, lane, pc);
-            stream_chunks<K, kChunk, Op::kSegChunks>(p.data, tp0, tp1, ps, pe, g.rl, g.rh, lane, &misc[7], op);
+            if constexpr (K >= 7) {
+                stream_chunks<K, kChunk, Op::kSegChunks>(p.data, tp0, tp1, ps, pe, g.rl, g.rh, lane, &misc[7], op);
+            } else {
+                constexpr int NWAVES = BLOCK / 64;
+                const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+                const int64_t per = (tp1 - tp0 + NWAVES - 1) / NWAVES;
+                const int64_t a0 = tp0 + (int64_t)wave * per;
+                const int64_t a1 = (a0 + per) < tp1 ? (a0 + per) : tp1;
+                stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);
+            }
             if constexpr (HM == 3) {
                 const uint32_t wsum = wave_sum(op.nwin);
                 if (lane == 0) atomicAdd(&misc[3], wsum);
