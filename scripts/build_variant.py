@@ -33,15 +33,19 @@ def main():
     H = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-fvisibility=hidden", "-std=c++17",
          "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc")]
     objs = []
-    for f, src in patched.items():
+    H = H[:-1] + ["-I" + vdir] + H[-1:]  # patched headers (.h) ahead of csrc/
+    for f, src in patched.items():  # every patched file first: a patched header is seen by all of them
+        open(os.path.join(vdir, f), "w").write(src)
+    for f in patched:
         tmp = os.path.join(vdir, f)
-        open(tmp, "w").write(src)
+        if f.endswith(".h"):  # (the patched .hip / .cpp files see it; the other objects keep csrc/'s)
+            continue
         obj = tmp.rsplit(".", 1)[0] + ".o"
         cc = H if f.endswith(".hip") else ["g++", "-O3", "-fPIC", "-fvisibility=hidden", "-std=c++17",
                                            "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"] + H[-2:]
         subprocess.check_call(cc + ["-c", tmp, "-o", obj])
         objs.append(obj)
-    done = {f.rsplit(".", 1)[0] + ".o" for f in patched}
+    done = {f.rsplit(".", 1)[0] + ".o" for f in patched if not f.endswith(".h")}
     others = sorted(os.path.join(PKG, "build", f) for f in os.listdir(os.path.join(PKG, "build"))
                     if f.startswith("kmc_") and f.endswith(".o") and f not in done)
     out = os.path.join(PKG, "lib", "variants", "libkmc_%s.so" % name)

@@ -33,19 +33,20 @@ def build():
         "__device__ unsigned long long g_dprof[1024][%d];\n"
         "#define TSW(i) (g_dprof[blockIdx.x][(i)] = __builtin_amdgcn_s_memrealtime())\n"
         "template <int K, int R, int HM, int BLOCK>\nstruct DenseOp {" % NSLOT)
-    rep("            if ((i % kHm3Scan) == kHm3Scan - 1 && i + 1 < per) {\n                lds_barrier();\n"
-        "                p16_scan<BLOCK, 32768u>(pc);\n                lds_barrier();\n",
-        "            if ((i % kHm3Scan) == kHm3Scan - 1 && i + 1 < per) {\n"
-        "                if ((threadIdx.x & 63) == 0 && i / kHm3Scan < 12)\n"
-        "                    TSW(48 + 16 * (i / kHm3Scan) + (threadIdx.x >> 6));\n"
-        "                lds_barrier();\n                p16_scan<BLOCK, 32768u>(pc);\n                lds_barrier();\n"
-        "                if (threadIdx.x == 0 && i / kHm3Scan < 12) TSW(240 + i / kHm3Scan);\n")
+    rep("    uint32_t nwin = 0u;  // HM 3: windows this lane added\n",
+        "    uint32_t nwin = 0u;  // HM 3: windows this lane added\n    int pseg = 0;\n")
+    rep("        if constexpr (HM == 3) {\n            lds_barrier();\n            p16_scan<BLOCK, 32768u>(pc);\n"
+        "            lds_barrier();\n        }\n",
+        "        if constexpr (HM == 3) {\n"
+        "            if ((threadIdx.x & 63) == 0 && pseg < 12) TSW(48 + 16 * pseg + (threadIdx.x >> 6));\n"
+        "            lds_barrier();\n            p16_scan<BLOCK, 32768u>(pc);\n            lds_barrier();\n"
+        "            if (threadIdx.x == 0 && pseg < 12) TSW(240 + pseg);\n            ++pseg;\n        }\n")
     rep("    if (tb < te) {\n        const int64_t R0",
         "    if (tid == 0) TSW(0);\n    if (tb < te) {\n        const int64_t R0")
     rep("        P16Ctx pc;\n", "        if (tid == 0) TSW(1);\n        P16Ctx pc;\n")
-    rep("            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);\n",
-        "            stream_tiles<K>(p.data, a0, a1, per, ps, pe, g.rl, g.rh, lane, op);\n"
-        "            if (lane == 0 && npieces < 2) TSW(2 + 16 * npieces + wave);\n")
+    rep("                stream_chunks<K, kChunk, Op::kSegChunks>(p.data, tp0, tp1, ps, pe, g.rl, g.rh, lane, &misc[7], op);\n",
+        "                stream_chunks<K, kChunk, Op::kSegChunks>(p.data, tp0, tp1, ps, pe, g.rl, g.rh, lane, &misc[7], op);\n"
+        "                if (lane == 0 && npieces < 2) TSW(2 + 16 * npieces + (tid >> 6));\n")
     rep("            const bool entire = (ps == ca) && (pe == ce);\n",
         "            if (tid == 0 && npieces < 2) TSW(34 + 3 * npieces);\n"
         "            const bool entire = (ps == ca) && (pe == ce);\n")
@@ -54,7 +55,10 @@ def build():
         "    if (tid == 0) {\n        TSW(40);\n        g_dprof[blockIdx.x][41] = (unsigned long long)(tb < te ? 1 : 0);\n"
         "        p.slot_rec[2 * w] = slot0;")
     src += ('\nextern "C" __attribute__((visibility("default"))) int kmc_denseprof_read(unsigned long long *out) {\n'
-            '    return hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_dprof), sizeof(kmc::g_dprof)) != hipSuccess;\n}\n')
+            '    return hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_dprof), sizeof(kmc::g_dprof)) != hipSuccess;\n}\n'
+            'extern "C" __attribute__((visibility("default"))) int kmc_denseprof_clear() {\n'
+            '    std::vector<unsigned long long> z(sizeof(kmc::g_dprof) / 8, 0ull);\n'
+            '    return hipMemcpyToSymbol(HIP_SYMBOL(kmc::g_dprof), z.data(), sizeof(kmc::g_dprof)) != hipSuccess;\n}\n')
     os.makedirs(os.path.join(PKG, "build", "v"), exist_ok=True)
     os.makedirs(os.path.dirname(VLIB), exist_ok=True)
     tmp = os.path.join(PKG, "build", "v", "kmc_dense_prof.hip")
@@ -107,6 +111,10 @@ def run(worlds, steps):
             kmc.count_dense_ex(args, stream)
         torch.cuda.synchronize()
         buf = np.zeros((1024, NSLOT), np.uint64)
+        assert lib.kmc_denseprof_clear() == 0
+        for _ in range(2):
+            kmc.count_dense_ex(args, stream)
+        torch.cuda.synchronize()
         assert lib.kmc_denseprof_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
         used = buf[:, 41] == 1
         b = buf[used].astype(np.int64)
