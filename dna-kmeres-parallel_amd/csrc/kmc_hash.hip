@@ -1181,8 +1181,14 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         const uint64_t nn = ne0 - nb0 <= (lim < (uint64_t)C::kCap ? lim : (uint64_t)C::kCap) ? ne0 - nb0 : 0;
         if ((uint64_t)tid * 16u < nn) {
             const uint64_t a = (uint64_t)(p.ent + nb0 + (uint64_t)tid * 16u);
-            asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(a), "s"(lds_off(&S.pfs[0]))
-                         : "m0", "memory");
+            // (m0, which the compiler reserves, is saved in an SGPR of our own and put
+            // back; s_nop 0: the wait state between an SALU write of m0 and the LDS-DMA
+            // that reads it)
+            uint32_t m0s;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(m0s)
+                         : "v"(a), "s"(lds_off(&S.pfs[0]))
+                         : "memory");
         }
     }
     if (tid == 0) {
