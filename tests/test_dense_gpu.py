@@ -166,6 +166,38 @@ def test_dense_random_vs_oracle(kmc, oracle, cuda, k):
     np.testing.assert_array_equal(inv, exp_inv)
 
 
+@pytest.mark.parametrize("k", [7, 8])
+def test_dense_chunk_boundaries_vs_oracle(kmc, oracle, cuda, k):
+    """k >= 7 hands a piece's tiles to the waves in 16-tile chunks (16 KiB) from a
+    workgroup counter; the halo of a chunk's last tile is loaded apart.  ~48 MB, so
+    every workgroup's range holds many chunks: records ending on and around chunk
+    edges (16 KiB multiples -8 .. +7), pieces shorter than one chunk, invalid bytes
+    on both sides of chunk edges, and window ranges (shards) cutting chunks."""
+    import torch
+    rng = np.random.default_rng(7070 + k)
+    lens = [16384 * m + d for m in (1, 2, 5, 33) for d in (-8, -1, 0, 1, 7)]
+    lens += [5, 16383, 3 * 16384 + 1023, 6_000_000, 10_000_001, 4096 * 37 + 11]
+    lens += list(rng.integers(1, 200_000, size=40)) + [12_000_000, 16_000_000]
+    rng.shuffle(lens)
+    data, idx = random_records(rng, lens, 0.0005, 0.0005, 0.0)
+    # invalid bytes right at chunk edges of the buffer (and one past, one before)
+    edges = np.arange(16384, data.size - 16, 16384 * 7)
+    for off in (-1, 0, 1):
+        data[edges + off] = np.uint8(ord("N"))
+    data[idx[1:] - 1] = 0  # (record terminators stay)
+    got, inv = run_dense(kmc, cuda, data, idx, k)
+    exp, exp_inv = oracle.count_dense(data, idx, k)
+    np.testing.assert_array_equal(got, exp)
+    np.testing.assert_array_equal(inv, exp_inv)
+    d, di = dev(data, cuda), dev(idx, cuda)
+    out = torch.empty((1 << (2 * k), idx.size - 1), dtype=torch.int32, device=cuda)
+    for lo, hi in ((16384 * 3 - 5, 16384 * 900 + 3), (1, data.size // 2 + 16384 - 1), (data.size // 3, data.size)):
+        kmc.count_dense_ex(kmc.dense_args(d, di, k, out.view(-1), read=(lo, min(hi + k - 1, data.size)), win=(lo, hi)))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), oracle.count_dense(data, idx, k, win=(lo, hi))[0],
+                                      err_msg="window range [%d, %d)" % (lo, hi))
+
+
 @pytest.mark.parametrize("k", [9, 10, 11, 12, 13])
 def test_radix_k9_13_vs_oracle(kmc, oracle, cuda, k):
     """9 <= k <= 13: the radix-partitioned path (67 M bins per record at k = 13)."""
