@@ -1,6 +1,7 @@
 """Diagnostic (round 4): where K4s's time goes, per phase of sort_list.
 
-Builds lib/variants/libkmc_k4sprof.so from the current kmc_hash.hip with clock
+Builds lib/variants/libkmc_k4sprof.so from the current kmc_hash.hip (round 5: the
+direct-output instances, with the reservation + write-out tail as a phase) with clock
 reads (s_memtime) patched in at the phase boundaries of sort_list (wave 0 of each
 workgroup, accumulated in registers over its lists, one device add per workgroup
 at the end) -- the product source carries none of it.  `--build` on the build host;
@@ -15,7 +16,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "dna-kmeres-parallel_amd")
 VLIB = os.path.join(PKG, "lib", "variants", "libkmc_k4sprof.so")
-PH = ["load+A", "rank+B", "scan+C1C2", "scatter", "D", "pairwise", "E", "hot"]
+PH = ["load+A", "rank+B", "scan+C1C2", "scatter", "D", "pairwise", "E", "hot", "tail"]
 
 
 def build():
@@ -25,10 +26,10 @@ def build():
         nonlocal src
         assert src.count(a) == 1, a
         src = src.replace(a, b)
-    rep("template <class C>\n__device__ __forceinline__ void sort_list(",
+    rep("template <class C, bool DIRECT>\n__device__ __forceinline__ void sort_list(",
         "__device__ unsigned long long g_k4s_prof[2][10];\n"
         "#define TS(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); acc[i] += _t - tp; tp = _t; } while (0)\n"
-        "template <class C>\n__device__ __forceinline__ void sort_list(")
+        "template <class C, bool DIRECT>\n__device__ __forceinline__ void sort_list(")
     rep("uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0) {",
         "uint32_t n, const uint64_t *nxt, uint64_t &nb0, uint64_t &ne0, unsigned long long (&acc)[10]) {\n"
         "    unsigned long long tp = __builtin_amdgcn_s_memtime();\n    acc[9] += 1;")
@@ -38,24 +39,29 @@ def build():
     rep("    lds_barrier();  // C2: slot starts\n", "    lds_barrier();  // C2: slot starts\n    TS(2);\n")
     rep("    lds_barrier();  // D: the keys of the failing slots sorted by slot\n",
         "    TS(3);\n    lds_barrier();  // D: the keys of the failing slots sorted by slot\n    TS(4);\n")
-    rep("    lds_barrier();  // E: every key emitted\n", "    TS(7);\n    lds_barrier();  // E: every key emitted\n")
     rep("    if (nhot) lds_barrier();", "    TS(5);\n    if (nhot) lds_barrier();")
-    rep("    if (tid == 0) p.ndist[l] = S.out;\n}", "    if (tid == 0) p.ndist[l] = S.out;\n    TS(6);\n}")
-    rep("                           nb0, ne0);\n    }\n}",
-        "                           nb0, ne0, acc);\n    }\n"
-        "    if (threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[1][i], acc[i]);\n}")
-    rep("    const int64_t nl = (int64_t)*p.nbig;\n", "    const int64_t nl = (int64_t)*p.nbig;\n    unsigned long long acc[10] = {};\n")
-    rep("        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0);",
-        "        sort_list<SortSmall>(p, S, l, b0, e0, n, nxt, nb0, ne0, acc);")
+    rep("    lds_barrier();  // E: every key emitted\n",
+        "    TS(7);\n    lds_barrier();  // E: every key emitted\n    TS(6);\n")
+    rep("    } else {\n        if (tid == 0) p.ndist[l] = S.out;\n    }\n}",
+        "        TS(8);\n    } else {\n        if (tid == 0) p.ndist[l] = S.out;\n    }\n}")
+    rep("        sort_list<SortSmall, DIRECT>(p, S, l, b0, e0, n, nxt, nb0, ne0);",
+        "        sort_list<SortSmall, DIRECT>(p, S, l, b0, e0, n, nxt, nb0, ne0, acc);")
     rep("    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n",
         "    uint64_t b0 = 0, e0 = 0;  // this list's bounds (the previous one loaded them)\n    unsigned long long acc[10] = {};\n")
     rep("        b0 = nb0;\n        e0 = ne0;\n    }\n}",
-        "        b0 = nb0;\n        e0 = ne0;\n    }\n    if (threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[0][i], acc[i]);\n}")
+        "        b0 = nb0;\n        e0 = ne0;\n    }\n"
+        "    if (DIRECT && threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[0][i], acc[i]);\n}")
+    rep("    const int64_t nl = DIRECT ? (int64_t)p.dist_off[p.l_hi] : (int64_t)*p.nbig;\n",
+        "    const int64_t nl = DIRECT ? (int64_t)p.dist_off[p.l_hi] : (int64_t)*p.nbig;\n    unsigned long long acc[10] = {};\n")
+    rep("                                   in < nl ? p.big + 3 * in + 1 : nullptr, nb0, ne0);\n    }\n}",
+        "                                   in < nl ? p.big + 3 * in + 1 : nullptr, nb0, ne0, acc);\n    }\n"
+        "    if (DIRECT && threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[1][i], acc[i]);\n}")
     src += ('\nextern "C" __attribute__((visibility("default"))) int kmc_k4sprof_read(unsigned long long *out) {\n'
             '    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_k4s_prof), sizeof(kmc::g_k4s_prof)) != hipSuccess) return 1;\n'
             '    static const unsigned long long z[20] = {};\n'
             '    return hipMemcpyToSymbol(HIP_SYMBOL(kmc::g_k4s_prof), z, sizeof(z)) != hipSuccess;\n}\n')
     os.makedirs(os.path.join(PKG, "build", "v"), exist_ok=True)
+    os.makedirs(os.path.dirname(VLIB), exist_ok=True)
     tmp = os.path.join(PKG, "build", "v", "kmc_hash_k4sprof.hip")
     open(tmp, "w").write(src)
     H = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-fvisibility=hidden", "-std=c++17",
@@ -92,7 +98,7 @@ def run():
     for inst, name in ((0, "common"), (1, "big")):
         v = list(out[10 * inst:10 * inst + 10])
         nl = v[9]
-        tot = sum(v[:8])
+        tot = sum(v[:9])
         print("%s: %d lists, %.0f cycles per list (wave 0)" % (name, nl, tot / max(nl, 1)))
         for i, ph in enumerate(PH):
             print("   %-10s %8.0f cycles  %5.1f %%" % (ph, v[i] / max(nl, 1), 100.0 * v[i] / max(tot, 1)))
