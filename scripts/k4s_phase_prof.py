@@ -56,6 +56,31 @@ def build():
     rep("                                   in < nl ? p.big + 3 * in + 1 : nullptr, nb0, ne0);\n    }\n}",
         "                                   in < nl ? p.big + 3 * in + 1 : nullptr, nb0, ne0, acc);\n    }\n"
         "    if (DIRECT && threadIdx.x == 0) for (int i = 0; i < 10; ++i) atomicAdd(&g_k4s_prof[1][i], acc[i]);\n}")
+    # crowded slots: per size class of m (9-16, 17-64, 65-256, 257-1024, > 1024 keys) the
+    # slots, their distinct keys and the cycles the wave spent on them
+    rep("    for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kBlk / 64) {\n"
+        "        const uint32_t sw = S.sc[S.hot[hs]];\n"
+        "        const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);\n",
+        "    for (uint32_t hs = (uint32_t)wv; hs < nhot; hs += kBlk / 64) {\n"
+        "        const uint32_t sw = S.sc[S.hot[hs]];\n"
+        "        const uint32_t a = sw & 0xFFFFu, e = a + slot_count(sw);\n"
+        "        const unsigned long long t_s0 = __builtin_amdgcn_s_memtime();\n"
+        "        const uint32_t m_s = e - a;\n"
+        "        const int cls = m_s <= 16 ? 0 : m_s <= 64 ? 1 : m_s <= 256 ? 2 : m_s <= 1024 ? 3 : 4;\n")
+    rep("            if (last) break;\n            c = nx;\n            piv = S.sk[nx];  // (not marked: a value other than piv's)\n        }\n",
+        "            if (last) break;\n            c = nx;\n            piv = S.sk[nx];  // (not marked: a value other than piv's)\n        }\n"
+        "        if (lane == 0) {\n"
+        "            atomicAdd(&g_k4s_slots[C::kCap == kSortCapBigCfg ? 1 : 0][cls][0], 1ull);\n"
+        "            atomicAdd(&g_k4s_slots[C::kCap == kSortCapBigCfg ? 1 : 0][cls][1], (unsigned long long)nd);\n"
+        "            atomicAdd(&g_k4s_slots[C::kCap == kSortCapBigCfg ? 1 : 0][cls][2], __builtin_amdgcn_s_memtime() - t_s0);\n"
+        "            atomicAdd(&g_k4s_slots[C::kCap == kSortCapBigCfg ? 1 : 0][cls][3], (unsigned long long)m_s);\n"
+        "        }\n")
+    rep("__device__ unsigned long long g_k4s_prof[2][10];\n",
+        "__device__ unsigned long long g_k4s_prof[2][10];\n__device__ unsigned long long g_k4s_slots[2][5][4];\n")
+    src += ('\nextern "C" __attribute__((visibility("default"))) int kmc_k4sprof_slots(unsigned long long *out) {\n'
+            '    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_k4s_slots), sizeof(kmc::g_k4s_slots)) != hipSuccess) return 1;\n'
+            '    static const unsigned long long z[40] = {};\n'
+            '    return hipMemcpyToSymbol(HIP_SYMBOL(kmc::g_k4s_slots), z, sizeof(z)) != hipSuccess;\n}\n')
     src += ('\nextern "C" __attribute__((visibility("default"))) int kmc_k4sprof_read(unsigned long long *out) {\n'
             '    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmc::g_k4s_prof), sizeof(kmc::g_k4s_prof)) != hipSuccess) return 1;\n'
             '    static const unsigned long long z[20] = {};\n'
@@ -95,6 +120,14 @@ def run():
         torch.cuda.synchronize()
         del r
         assert lib.kmc_k4sprof_read(out) == 0
+    sl = (ctypes.c_ulonglong * 40)()
+    assert lib.kmc_k4sprof_slots(sl) == 0
+    for inst, name in ((0, "common"), (1, "big")):
+        for c, cn in enumerate(("9-16", "17-64", "65-256", "257-1024", ">1024")):
+            q = sl[inst * 20 + c * 4:inst * 20 + c * 4 + 4]
+            if q[0]:
+                print("%s crowded slots m %-9s %9d slots, %6.2f distinct keys, %7.0f keys, %8.0f cycles per slot; "
+                      "%.0f cycles per list" % (name, cn, q[0], q[1] / q[0], q[3] / q[0], q[2] / q[0], q[2] / 8.0))
     for inst, name in ((0, "common"), (1, "big")):
         v = list(out[10 * inst:10 * inst + 10])
         nl = v[9]
