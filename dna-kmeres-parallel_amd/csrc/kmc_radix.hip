@@ -17,7 +17,7 @@
 //   R5 place    transpose stage into sum[s + ld*code] (k-mer-major, coalesced)
 //
 // Sampled mode (large inputs: >= 4096 windows per (record, bucket, workgroup) on
-// average, e.g. C3): R1's full read of the input is replaced by a 1-in-8 tile sample
+// average, e.g. C3): R1's full read of the input is replaced by a 1-in-16 tile sample
 // (S1, the same kernel with sample_tiles) whose weighted counts size one region
 // per (s, b, w) with a margin (radix_cap_kernel); R2 scans the capacities, R3
 // writes into the regions and records each one's fill in cnt, R4 walks a list as
@@ -78,7 +78,7 @@ struct RParams {
     int32_t *sum;
     int64_t ld;
     int32_t *invalid;
-    // sampled mode (radix_count_kernel<SAMPLE>): regions sized from a 1-in-8 tile sample
+    // sampled mode (radix_count_kernel<SAMPLE>): regions sized from a 1-in-16 tile sample
     uint32_t *capv;      // [n][nbk][G] region capacities (multiples of 32); null: exact offsets
     uint32_t *flag;      // overflow lists full (or capacities beyond ent_cap): exact rerun
     const uint32_t *gate;  // non-null: the kernel runs only if *gate != 0 (the exact rerun)
@@ -123,7 +123,9 @@ struct RCountOp {
 // with weight = the stride, kSampleFlight tiles in flight.  A sampled tile has no next tile:
 // the windows of lane 63 that need its halo are skipped (1.2 % of them at k = 13),
 // which the capacities' margin covers.
-constexpr int kSampleStride = 8, kSampleAll = 16, kSampleFlight = 8;
+constexpr int kSampleStride = 16, kSampleAll = 16, kSampleFlight = 8;
+constexpr int kSampleLog = __builtin_ctz(kSampleStride);
+static_assert((kSampleStride & (kSampleStride - 1)) == 0, "the phase takes log2(stride) hash bits");
 template <int K, class Op>
 __device__ __forceinline__ void sample_tiles(const char *__restrict__ data, int64_t a0, int64_t a1, int64_t ps,
                                              int64_t pe, int64_t rl, int64_t rh, int lane, uint32_t seed, Op &op) {
@@ -131,7 +133,7 @@ __device__ __forceinline__ void sample_tiles(const char *__restrict__ data, int6
     if (len <= 0) return;
     const int stride = len <= kSampleAll ? 1 : kSampleStride;
     op.wgt = (uint32_t)stride;
-    const int64_t phase = stride == 1 ? 0 : (int64_t)((seed * 0x9E3779B1u) >> 29);
+    const int64_t phase = stride == 1 ? 0 : (int64_t)((seed * 0x9E3779B1u) >> (32 - kSampleLog));
     for (int64_t t = a0 + phase; t < a1; t += kSampleFlight * stride) {
         uint4 r[kSampleFlight];
 #pragma unroll
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(1024) void radix_count_kernel(RParams p) {
 
 // Sampled mode: the region capacity of every (s, b, w) from the weighted sample
 // count c (an estimate of the region's entries): 1.05 c + 6 sigma + 64, sigma =
-// sqrt(8 c) the Poisson error of a 1-in-8 sample, rounded up to 32 entries (whole
+// sqrt(16 c) the Poisson error of a 1-in-16 sample, rounded up to 32 entries (whole
 // 64-byte segments: regions stay segment-aligned) and at most the piece's windows;
 // 0 where workgroup w holds no piece of record s (whatever cnt held there).  Clears
 // cnt: R3 writes the fills, an exact rerun's R1 the counts.
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(256) void radix_cap_kernel(RParams p) {
         uint32_t cap = 0u;
         if (tb < te && ps < pe) {
             const float c = (float)p.cnt[i];
-            const float x = (1.05f * c + 6.0f * sqrtf(8.0f * c) + 64.0f) * p.cap_scale;
+            const float x = (1.05f * c + 6.0f * sqrtf((float)kSampleStride * c) + 64.0f) * p.cap_scale;
             const int64_t pmax = (pe - ps + 31) & ~(int64_t)31;
             cap = x >= (float)pmax ? (uint32_t)pmax : (((uint32_t)x + 31u) & ~31u);
         }
@@ -1020,13 +1022,14 @@ std::mutex r_mu;
 std::vector<int> r_cus;  // CUs per device
 
 // Partition offsets (kmc_diag_radix_mode): 0 = auto, 1 = exact (R1 count + scan),
-// 2 = sampled (regions sized from a 1-in-8 tile sample, exact rerun on overflow);
+// 2 = sampled (regions sized from a 1-in-16 tile sample, exact rerun on overflow);
 // cap_scale multiplies the sampled capacities (test hook: < 1 forces the rerun).
 int g_radix_mode = 0;
 float g_cap_scale = 1.0f;
 
 // Sampled mode pays when the lists are long: it replaces R1's full read of the
-// input by a 1-in-8 sample (C3: R1 1.95 -> 0.42 ms), but R4 then sets up G regions
+// input by a 1-in-16 sample (C3: R1 1.95 -> 0.21 ms; 1-in-8 0.42, 1-in-32 0.12 ms
+// but R3 + R4 +0.1-0.2 ms with the wider regions, same box), but R4 then sets up G regions
 // per list and walks them (C3: +0.1-0.3 ms over 10 240 lists of ~1 M entries; C3R,
 // 25 600 lists of ~120 K entries: +0.6 ms, more than its R1 saving).
 constexpr double kSampledMinPerList = 256.0 * 1024.0;
@@ -1074,9 +1077,9 @@ int run_radix(const kmc_dense_args *a, int64_t ibias, hipStream_t st, bool size_
     }
     const bool sampled = G <= kMaxRegions &&
                          (mode == 2 || (mode == 0 && win >= kSampledMinPerList * (double)n * (double)NBK));
-    // sampled capacities: sum over regions of 1.05 c + 6 sqrt(8 c) + 64 (+ 31 rounding),
+    // sampled capacities: sum over regions of 1.05 c + 6 sqrt(16 c) + 64 (+ 31 rounding),
     // c summing to the windows; Cauchy-Schwarz bounds the square roots
-    const int64_t ent_cap = sampled ? (int64_t)(1.05 * win + 95.0 * regions + 6.0 * std::sqrt(8.0 * win * regions) + 64.0)
+    const int64_t ent_cap = sampled ? (int64_t)(1.05 * win + 95.0 * regions + 6.0 * std::sqrt((double)kSampleStride * win * regions) + 64.0)
                                     : (int64_t)win;
     // overflow lists: 1/32 of the windows in all (past that, the exact rerun)
     const uint32_t ovf_cap = (uint32_t)std::min<double>(std::max<double>(4096.0, win / 32.0 / G), 1 << 30);

@@ -250,7 +250,7 @@ def radix_mode(kmc):
 @pytest.mark.parametrize("k", [9, 10, 11, 12, 13])
 @pytest.mark.parametrize("scale", [1.0, 0.97, 0.25])
 def test_radix_sampled_regions_vs_oracle(kmc, oracle, cuda, radix_mode, k, scale):
-    """The sampled partition (C3's path): R1 replaced by a 1-in-8 tile sample that
+    """The sampled partition (C3's path): R1 replaced by a 1-in-16 tile sample that
     sizes a region per (record, bucket, workgroup), R3 writing into the regions and
     R4 walking them.  scale 1: regions fit; 0.97: a few overflow, 0.25: most do --
     either way the device-side exact rerun must give the oracle's counts.  Random
