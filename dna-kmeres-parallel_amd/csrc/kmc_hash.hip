@@ -8,8 +8,8 @@
 //
 // Hash-partitioned counting, so that no table lives in HBM and no k-mer costs a
 // device-scope atomic.  The input walks partition a window by m = key x C (one
-// multiply, invertible); the lists hold h = fmix62(key) (a bijection of 62-bit
-// values; only the distinct keys are unmixed, by K5).  Record r has 2^lg_r lists (top lg_r
+// multiply, invertible); the lists hold h = feistel(key) (one Feistel round on
+// the 62-bit key, its own inverse: the distinct keys are mapped back on output).  Record r has 2^lg_r lists (top lg_r
 // bits of m, about 4 K windows each, lg_r <= 15), grouped in 2^lgc_r coarse
 // buckets (top lgc_r = min(lg_r, 7) bits):
 //   K1 count    workgroups walk contiguous chunk ranges record piece by record
@@ -53,7 +53,7 @@
 namespace kmc {
 namespace {
 
-constexpr uint64_t kEmptyH = ~0ull;  // no list value: those are fmix62 outputs, < 2^62
+constexpr uint64_t kEmptyH = ~0ull;  // no list value: those are feistel outputs, < 2^62
 constexpr int kWalkBlock = 1024;             // K1 / K3a / K3b threads per workgroup
 constexpr int kMaxLg = 15;                   // at most 32 768 lists per record (K1's LDS counters)
 constexpr int kCoarseLg = 7;                 // at most 128 coarse buckets per record
@@ -133,40 +133,36 @@ struct HParams {
 };
 
 // Partition value of a key: K1 / K3a / K3b bucket and list by its top bits.  A
-// multiplicative hash (one 64-bit multiply, invertible) instead of fmix62 in
-// the two input walks; K3b (or K3a for single-list buckets) turns it into
-// fmix62(key) when writing the lists, which is what K4 hashes and K5 unmixes.
+// multiplicative hash (one 64-bit multiply, invertible) in the two input walks;
+// K3b (or K3a for single-list buckets) turns it into feistel(key) when writing the
+// lists, which is what K4s / K4 hash and the output maps back to the key.
 constexpr uint64_t kMulC = 0x9E3779B97F4A7C15ull, kMulCinv = 0xF1DE83E19937733Dull;
 __device__ __forceinline__ uint64_t part_of(uint64_t key);
 __device__ __forceinline__ uint64_t list_value(uint64_t m);
 
-// MurmurHash3's fmix64 rounds on 62-bit values (a k <= 31 key): a bijection of [0, 2^62) --
-// multiplication by an odd constant mod 2^62, and x ^= x >> 31, which is its own
-// inverse on 62 bits -- so a list value leaves the top two bits free, and K4s / K4
-// emit it with the count tag there: the inverse (unmix62, ~20 VALU ops per key)
-// runs in the memory-bound place kernel, not in the issue-bound counting kernels.
+// A k <= 31 key uses at most 62 bits, and so does its list value (below): the top
+// two bits carry the count tag of the pair format.
 constexpr uint64_t kM62 = (1ull << 62) - 1ull;
-__device__ __forceinline__ uint64_t fmix62(uint64_t h) {
-    h ^= h >> 31;
-    h = (h * 0xFF51AFD7ED558CCDull) & kM62;
-    h ^= h >> 31;
-    h = (h * 0xC4CEB9FE1A85EC53ull) & kM62;
-    h ^= h >> 31;
-    return h;
-}
-__device__ __forceinline__ uint64_t unmix62(uint64_t h) {  // inverse of fmix62
-    h ^= h >> 31;
-    h = (h * 0x9CB4B2F8129337DBull) & kM62;  // (inverses mod 2^64 are inverses mod 2^62)
-    h ^= h >> 31;
-    h = (h * 0x4F74430C22A54005ull) & kM62;
-    h ^= h >> 31;
-    return h;
+
+// One Feistel round on a key's 62 bits: the low 17 bits XORed with the top 17 bits
+// of (key >> 17) * kFeiC.  The high 45 bits pass unchanged, so the map is its own
+// inverse (~8 VALU ops either way).  The low 17 bits are what K4s (slot + sub) and
+// K4 (slot) hash: two keys that agree on their first 22-23 bases differ there, the
+// others collide at random.  Round 5: it replaces MurmurHash3's fmix64 rounds on
+// 62 bits, whose ~20-op inverse ran in K4s's write-out once the place kernel was
+// gone (a timing-only build without it: C4 -1.05, C4R -0.7 ms): same box, C4
+// 33.1-33.2 -> 32.3-32.4 ms, C4R 44.2-44.3 -> 43.6-44.0 ms
+// (profiles/r05ar_feistel_list_value_ab.txt).
+constexpr uint64_t kFeiC = 0x9FB21C651E98DF25ull;
+__device__ __forceinline__ uint64_t feistel(uint64_t x) {
+    const uint64_t hi = x >> 17;
+    return x ^ ((hi * kFeiC) >> 47);
 }
 
 __device__ __forceinline__ uint64_t part_of(uint64_t key) { return key * kMulC; }
 
-__device__ __forceinline__ uint64_t list_value(uint64_t m) {  // partition value -> fmix62(key)
-    return fmix62(m * kMulCinv);
+__device__ __forceinline__ uint64_t list_value(uint64_t m) {  // partition value -> list value
+    return feistel(m * kMulCinv);
 }
 
 // LE 2-bit code (first base in the low bits, the dense path's order) -> MSB-first
@@ -878,7 +874,8 @@ __device__ __forceinline__ void probe_staged(K4Lds &L, int wv, uint32_t nq, uint
 // list bits), so that splitting pass q of P gives passes 2q and 2q + 1 of 2P
 __device__ __forceinline__ uint32_t pass_of(unsigned long long h, uint32_t P) {
     constexpr int kBits = kPassTop - 32;
-    return (uint32_t)((((h >> 32) & ((1ull << kBits) - 1ull)) * (uint64_t)P) >> kBits);
+    const uint64_t x = h * 0xD6E8FEB86659FD93ull;  // (the list value's high bits are raw key bits)
+    return (uint32_t)((((x >> 32) & ((1ull << kBits) - 1ull)) * (uint64_t)P) >> kBits);
 }
 
 // The wave's keys of pass q / P, staged in its LDS queue and probed; a queue that
@@ -1408,7 +1405,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
                 const unsigned long long h = S.sk[a ? nsk + i : n + (i - na)];
                 const uint32_t cnt = a ? 1u : S.rc[i - na];
                 if (fin) {
-                    p.out_keys[g + i] = unmix62(h);
+                    p.out_keys[g + i] = feistel(h);
                     p.out_counts[g + i] = cnt;
                 } else {
                     emit_pair(p, g + i, h, cnt);
@@ -1493,7 +1490,7 @@ __global__ __launch_bounds__(256) void canon_place_kernel(HParams p) {
             const uint64_t i = i0 + 256u * u;
             if (i < m) {
                 const uint32_t tag = (uint32_t)(x[u] >> 62);
-                const uint64_t key = unmix62(x[u] & kM62);
+                const uint64_t key = feistel(x[u] & kM62);
                 const uint32_t cnt = tag < 3u ? tag + 1u : p.pc[src + i];
                 p.out_keys[dst + i] = key;
                 p.out_counts[dst + i] = cnt;
@@ -1584,7 +1581,7 @@ __global__ __launch_bounds__(256) void canon_fallback_kernel(HParams p) {
         for (uint64_t i = threadIdx.x; i < m; i += 256) {
             const unsigned long long x = p.pk[src + i];
             const uint32_t tag = (uint32_t)(x >> 62);
-            p.out_keys[dst + i] = unmix62(x & kM62);
+            p.out_keys[dst + i] = feistel(x & kM62);
             p.out_counts[dst + i] = tag < 3u ? tag + 1u : p.pc[src + i];
         }
     }

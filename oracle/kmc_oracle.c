@@ -268,7 +268,7 @@ int64_t oracle_count_canonical(const uint8_t *data, const int64_t *indices, int6
  *             sel_val and their counts, sorted ascending (a subset compared key by
  *             key with the GPU output restricted to the same predicate)
  * dg_hash is splitmix64's finaliser, unrelated to the GPU's partition multiply and
- * fmix62 list values (kmc_hash.hip), so the selected subset spans every list.
+ * feistel list values (kmc_hash.hip), so the selected subset spans every list.
  * Returns the number of selected distinct keys, or -1 when more than `cap`
  * selected windows occur.
  */

@@ -180,22 +180,17 @@ def test_canonical_crowded_list_deferred(kmc, oracle, cuda):
         assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "k=%d" % k)
 
 
-def _fmix62(h):
-    """fmix62 of kmc_hash.hip (uint64 arrays, wrapping multiplies)."""
-    m62 = np.uint64((1 << 62) - 1)
+def _list_value(key):
+    """The list value of kmc_hash.hip (feistel: uint64 arrays, wrapping multiplies):
+    K4s's slot and sub are its low 12 and next 4 bits."""
     with np.errstate(over="ignore"):
-        h = h ^ (h >> np.uint64(31))
-        h = (h * np.uint64(0xFF51AFD7ED558CCD)) & m62
-        h = h ^ (h >> np.uint64(31))
-        h = (h * np.uint64(0xC4CEB9FE1A85EC53)) & m62
-        h = h ^ (h >> np.uint64(31))
-    return h
+        return key ^ (((key >> np.uint64(17)) * np.uint64(0x9FB21C651E98DF25)) >> np.uint64(47))
 
 
 @pytest.mark.parametrize("nd", [9, 64, 65, 100])
 def test_canonical_crowded_slot_many_keys(kmc, oracle, cuda, nd):
     """A crowded K4s slot holding many distinct keys: nd distinct 31-mers whose
-    fmix62(canonical key) share the low 12 bits (one slot of the common instance's
+    list values (feistel of the canonical key) share the low 12 bits (one slot of the common instance's
     4 096), each written 1-5 times between N's, in a record short enough to be one
     list -- the crowded-slot rounds then find nd pivots in a slot of ~3 nd keys
     (over 128 keys: several chunk pairs per pass), and emit their results 64 at a
@@ -208,7 +203,7 @@ def test_canonical_crowded_slot_many_keys(kmc, oracle, cuda, nd):
     for q in range(k):  # reverse complement of the MSB-first 2-bit code
         rc |= (np.uint64(3) - ((codes >> np.uint64(2 * q)) & np.uint64(3))) << np.uint64(2 * (k - 1 - q))
     canon = np.minimum(codes, rc)
-    sel = np.flatnonzero((_fmix62(canon) & np.uint64(4095)) == 0)
+    sel = np.flatnonzero((_list_value(canon) & np.uint64(4095)) == 0)
     _, first = np.unique(canon[sel], return_index=True)
     pick = codes[sel[np.sort(first)][:nd]]
     assert pick.size == nd
@@ -229,7 +224,7 @@ def test_canonical_crowded_slot_many_keys(kmc, oracle, cuda, nd):
 
 def test_canonical_slot_distinctness_test_edges(kmc, oracle, cuda):
     """K4s proves a slot's keys distinct when the high half of its word -- one
-    2^sub per key, sub = bits 12-15 of fmix62(key) -- has as many bits set as the
+    2^sub per key, sub = bits 12-15 of the key's list value -- has as many bits set as the
     slot has keys.  Constructed edges, each group in a slot of its own of one
     list: 16 distinct keys on all 16 subs (the largest slot that passes); 2
     distinct keys on sub 15 (the sum carries out of the word: fails, pairwise
@@ -242,7 +237,7 @@ def test_canonical_slot_distinctness_test_edges(kmc, oracle, cuda):
     for q in range(k):
         rc |= (np.uint64(3) - ((codes >> np.uint64(2 * q)) & np.uint64(3))) << np.uint64(2 * (k - 1 - q))
     canon = np.minimum(codes, rc)
-    h = _fmix62(canon)
+    h = _list_value(canon)
     slot = (h & np.uint64(4095)).astype(np.int64)
     sub = ((h >> np.uint64(12)) & np.uint64(15)).astype(np.int64)
 
