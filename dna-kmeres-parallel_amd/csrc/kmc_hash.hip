@@ -1061,7 +1061,7 @@ using SortBig = SortCfg<1024, 12, kSortCapBigCfg, 13, 15232, 2048>;   // LDS: 1 
 constexpr int kSortBlock = SortSmall::kBlock;
 constexpr uint32_t kSortCap = SortSmall::kCap;
 constexpr uint32_t kSortCapBig = SortBig::kCap;
-constexpr uint32_t kSortMaxM = 8;                     // keys per slot handled by the pairwise dedup
+constexpr uint32_t kSortMaxM = 16;                    // keys per slot handled by the pairwise dedup
 constexpr uint32_t kHotMax = 128;                     // crowded slots per list handled by wave rounds
 
 template <class C>
@@ -1300,14 +1300,26 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
             first = e - a <= kSortMaxM;
             if (first) {
                 // the slot's keys read all at once (2 <= m <= kSortMaxM; past the slot:
-                // this key's own position, excluded below), not one round trip each
-#pragma unroll
-                for (uint32_t t = 0; t < kSortMaxM; ++t) {
+                // this key's own position, excluded below), not one round trip each --
+                // eight, and eight more only in a wave where some slot holds more
+                // (round 5: slots of 9-16 keys, repeats in C4R, compared here instead
+                // of in the crowded-slot rounds; same box C4R 43.7-43.9 -> 42.5-42.8 ms,
+                // C4 unchanged, profiles/r05av_k4s_pairwise_limit_ab.txt)
+                const auto cmp = [&](uint32_t t) {
                     const uint32_t q = a + t;
                     const unsigned long long x = S.sk[q < e ? q : pos];
                     if (q < e && q != pos && x == h) {
                         ++cnt;
                         first = first && q > pos;
+                    }
+                };
+#pragma unroll
+                for (uint32_t t = 0; t < 8; ++t) cmp(t);
+#pragma unroll
+                for (uint32_t t0 = 8; t0 < kSortMaxM; t0 += 8) {
+                    if (e - a > t0) {
+#pragma unroll
+                        for (uint32_t t = t0; t < t0 + 8; ++t) cmp(t);
                     }
                 }
             }

@@ -228,8 +228,10 @@ def test_canonical_slot_distinctness_test_edges(kmc, oracle, cuda):
     slot has keys.  Constructed edges, each group in a slot of its own of one
     list: 16 distinct keys on all 16 subs (the largest slot that passes); 2
     distinct keys on sub 15 (the sum carries out of the word: fails, pairwise
-    check); 9 keys on 9 subs, one of them written twice (fails, crowded); 8 keys,
-    two on one sub (fails, pairwise).  Counts against the oracle."""
+    check); 9 keys on 9 subs, one of them written twice (fails, pairwise: 10 keys,
+    the second tier of its reads); 8 keys, two on one sub (fails, pairwise); 3
+    keys written 5, 4 and 5 times (14 keys in one slot: pairwise, copies in both
+    tiers).  Counts against the oracle."""
     k = 31
     rng = np.random.default_rng(4242)
     codes = rng.integers(0, 1 << 62, size=1 << 22, dtype=np.uint64)
@@ -252,7 +254,8 @@ def test_canonical_slot_distinctness_test_edges(kmc, oracle, cuda):
     groups = [(keys_of(7, range(16)), [1] * 16),
               (keys_of(8, [15, 15]), [1, 1]),
               (keys_of(9, range(9)), [2] + [1] * 8),
-              (keys_of(10, [3, 3, 0, 1, 2, 4, 5, 6]), [1] * 8)]
+              (keys_of(10, [3, 3, 0, 1, 2, 4, 5, 6]), [1] * 8),
+              (keys_of(11, [0, 1, 2]), [5, 4, 5])]
     bases = np.frombuffer(b"ACGT", dtype=np.uint8)
     parts = []
     for ks, reps in groups:
@@ -264,7 +267,7 @@ def test_canonical_slot_distinctness_test_edges(kmc, oracle, cuda):
     data = np.concatenate([rec, data2])
     idx = np.concatenate([[0], rec.size + idx2]).astype(np.int64)
     exp = oracle.count_canonical(data, idx, k)
-    assert int(exp[2][1]) == 16 + 2 + 9 + 8
+    assert int(exp[2][1]) == 16 + 2 + 9 + 8 + 3
     assert_same(gpu_canon(kmc, cuda, data, idx, k), exp, "slot edges")
 
 
