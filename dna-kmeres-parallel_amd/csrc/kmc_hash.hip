@@ -1412,15 +1412,31 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         {
             const bool fin = S.mode != 0u;
             const unsigned long long g = S.gbase;
-            for (uint32_t i = (uint32_t)tid; i < Ds; i += kBlk) {
-                const bool a = i < na;
-                const unsigned long long h = S.sk[a ? nsk + i : n + (i - na)];
-                const uint32_t cnt = a ? 1u : S.rc[i - na];
-                if (fin) {
-                    p.out_keys[g + i] = feistel(h);
-                    p.out_counts[g + i] = cnt;
-                } else {
-                    emit_pair(p, g + i, h, cnt);
+            if (fin) {
+                // two loops -- the distinct slots' keys (count 1), then the results --
+                // instead of one with a per-pair select of source and count, on
+                // pointers set up once (round 5, same box: C4 32.5-32.6 -> 31.9-32.0 ms,
+                // C4R 42.6-42.7 -> 41.9-42.0 ms, profiles/r05ax_k4s_writeout_loops_ab.txt;
+                // the issue-bound tail pays for every VALU op per pair)
+                uint64_t *ko = p.out_keys + g;
+                uint32_t *co = p.out_counts + g;
+                const unsigned long long *sa = S.sk + nsk;
+                for (uint32_t i = (uint32_t)tid; i < na; i += kBlk) {
+                    ko[i] = feistel(sa[i]);
+                    co[i] = 1u;
+                }
+                const unsigned long long *sr = S.sk + n;
+                uint64_t *kr = ko + na;
+                uint32_t *cr = co + na;
+                for (uint32_t i = (uint32_t)tid; i < Ds - na; i += kBlk) {
+                    kr[i] = feistel(sr[i]);
+                    cr[i] = S.rc[i];
+                }
+            } else {
+                for (uint32_t i = (uint32_t)tid; i < Ds; i += kBlk) {
+                    const bool a = i < na;
+                    const unsigned long long h = S.sk[a ? nsk + i : n + (i - na)];
+                    emit_pair(p, g + i, h, a ? 1u : S.rc[i - na]);
                 }
             }
         }
