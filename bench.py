@@ -387,9 +387,10 @@ def main():
     # algorithmic bytes of one histogram launch on this GPU: its ASCII input bytes +
     # the int32 matrix it writes
     alg_bytes = (win_hi - win_lo) + 4 * nb * n_tot
-    kern_ms = sum(b.elapsed_time(e) for b, e in ev) / args.steps
+    step_ms = [b.elapsed_time(e) for b, e in ev]
+    kern_ms = sum(step_ms) / args.steps
     result = finalize(args, world, rank, backend, data, bufs[0], L, k, n_tot, (win_lo, win_hi), t1 - t0, kern_ms,
-                      alg_bytes, timer="cuda")
+                      alg_bytes, timer="cuda", step_ms=step_ms)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -435,34 +436,71 @@ def over_ranks(world, vals, device):
     return [float(v) for v in t.tolist()]
 
 
-def pmc_traffic(path, k, data_bytes):
+def dense_code_object_id(lib_path=None):
+    """Identity of the histogram kernel's build: sha256 (16 hex digits) of the gfx950
+    code object that holds count_dense_kernel inside libkmc.so's offload bundles
+    (one bundle per translation unit; the same sources and compiler give the same
+    bytes).  PMC summaries store the id of the build they measured, and the bench
+    line uses only entries whose id matches the library it ran (None: not found)."""
+    import hashlib
+    import struct
+    if lib_path is None:
+        import kmc
+        lib_path = kmc.LIB_PATH
+    try:
+        with open(lib_path, "rb") as f:
+            b = f.read()
+    except OSError:
+        return None
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    i = b.find(magic)
+    while i >= 0:
+        n = struct.unpack_from("<Q", b, i + 24)[0]
+        o = i + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", b, o)
+            o += 24
+            triple = b[o:o + tl]
+            o += tl
+            if b"gfx950" in triple and size:
+                co = b[i + off:i + off + size]
+                if b"count_dense_kernel" in co:
+                    return hashlib.sha256(co).hexdigest()[:16]
+        i = b.find(magic, i + len(magic))
+    return None
+
+
+def pmc_traffic(path, k, data_bytes, build_id):
     """HBM bytes per launch of the histogram kernel over a shard of data_bytes
     window bytes, measured by rocprofv3 PMC (profiles/pmc_*.json: one object or a
-    list of them, one per shard size); None when no measurement matches."""
-    if not path or not os.path.exists(path):
+    list of them, one per shard size) on the build `build_id`; None when no
+    measurement of this build matches (a counter of another build is never
+    reported as this run's traffic)."""
+    if not path or not os.path.exists(path) or build_id is None:
         return None
     with open(path) as f:
         pmc = json.load(f)
     for e in (pmc if isinstance(pmc, list) else [pmc]):
-        if e.get("k") == k and e.get("data_bytes") == data_bytes:
+        if e.get("k") == k and e.get("data_bytes") == data_bytes and e.get("build_id") == build_id:
             return e.get("hbm_bytes_per_launch")
     return None
 
 
-def lds_floor(path, k):
+def lds_floor(path, k, build_id):
     """The LDS-array roof of the k = 8 histogram (7 array cycles per
     wave-wide ds_add_u32, 72 % of them bank conflicts of random bins): the share of
     the kernel's shader cycles in which an average CU's LDS array is busy
     (SQ_LDS_IDX_ACTIVE / CUs / (GRBM_GUI_ACTIVE / 8), rocprofv3 PMC of this bench
     command, profiles/pmc_lds_k8_10gbase.json).  None when not measured."""
-    if k != 8 or not path or not os.path.exists(path):
+    if k != 8 or not path or not os.path.exists(path) or build_id is None:
         return None
     with open(path) as f:
         m = json.load(f)
-    return m if m.get("k") == k and "lds_busy_frac" in m else None
+    return m if m.get("k") == k and "lds_busy_frac" in m and m.get("build_id") == build_id else None
 
 
-def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed, kern_ms, alg_bytes, timer):
+def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed, kern_ms, alg_bytes, timer,
+             step_ms=None):
     """Everything after the timed region, at every N: the all-reduce timed alone,
     the max-over-ranks statistics, the reference CPU path on rank 0, and the JSON
     line (returned on rank 0, None elsewhere).  tests/test_multi.py runs it with
@@ -472,12 +510,17 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
     nb = 1 << (2 * k)
     dev = matrix.device
     ar_ms = measure_allreduce(matrix, args.allreduce_reps, timer) if world > 1 else 0.0
-    traffic = pmc_traffic(args.pmc, k, win_hi - win_lo)
+    build_id = dense_code_object_id() if timer == "cuda" else None
+    traffic = pmc_traffic(args.pmc, k, win_hi - win_lo, build_id)
     achieved_rank = alg_bytes / (kern_ms * 1e-3) / 1e9
+    # per-step histogram kernel times of this rank (HIP events): the spread shows a
+    # clock still ramping in the first timed steps
+    st = sorted(step_ms) if step_ms else [kern_ms]
+    med = st[len(st) // 2] if len(st) % 2 else 0.5 * (st[len(st) // 2 - 1] + st[len(st) // 2])
     # max over ranks of time-likes; min of achieved and of "traffic known" (as -x)
-    elapsed, kern_ms, ar_ms, neg_ach, neg_known, traffic_max = over_ranks(
+    elapsed, kern_ms, ar_ms, neg_ach, neg_known, traffic_max, k_med, k_min, k_max = over_ranks(
         world, [elapsed, kern_ms, ar_ms, -achieved_rank, -(1.0 if traffic is not None else 0.0),
-                float(traffic or 0.0)], dev)
+                float(traffic or 0.0), med, st[0], st[-1]], dev)
     achieved = -neg_ach
     traffic = traffic_max if -neg_known > 0.5 else None  # every rank's shard size was measured
 
@@ -525,7 +568,16 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
             "traffic": traffic,
             "kernel": "count_dense_kernel<%d> (HIP events around the histogram launch; slowest rank)" % k,
             "kernel_ms": kern_ms,
+            "kernel_ms_median": k_med,
+            "kernel_ms_min": k_min,
+            "kernel_ms_max": k_max,
+            "kernel_ms_how": "per timed step, HIP events around the histogram launch; kernel_ms is their mean "
+                             "(achieved / frac use it), median / min / max over the steps (each the slowest rank's)",
             "alg_bytes_per_launch": alg_bytes,
+            "build_id": build_id,
+            "traffic_how": ("HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE of this "
+                            "shard size, taken on the build whose code-object id is build_id (%s); null when no PMC "
+                            "entry of this build exists" % os.path.relpath(args.pmc, REPO)) if args.pmc else None,
             # the whole node: value x algorithmic bytes per k-mer of the job over N x peak
             "node_achieved": node_gbps,
             "node_peak": HBM_PEAK_GBPS * world,
@@ -542,7 +594,7 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
         },
     }
     # the roof that binds k = 8: the LDS array, not HBM
-    m = lds_floor(getattr(args, "pmc_lds", None), k)
+    m = lds_floor(getattr(args, "pmc_lds", None), k, build_id)
     if m is not None:
         result["roofline"].update({
             "binding": "lds",

@@ -16,8 +16,12 @@ extern "C" const char *kmc_error_string(int code) {
         case KMC_ERR_NO_DEVICE: return "no HIP device visible";
         case KMC_ERR_CAPACITY: return "output capacity smaller than the result";
         case KMC_ERR_RECORD_TOO_LONG: return "a record has 2^31 or more windows in one call: int32 counts could wrap";
+        case KMC_ERR_INTERNAL: return "a device-side bound check fired (library defect): outputs not valid";
         default: return hipGetErrorString(static_cast<hipError_t>(code));
     }
 }
 
-extern "C" int kmc_version(void) { return 100; }  // 0.1.0
+// 0.2.0: kmc_dense_args gained its trailing `status` field (round 5) and
+// KMC_ERR_INTERNAL was added (round 6); a caller built against the 0.1 header
+// passes the shorter struct and must check kmc_version() >= 200 first.
+extern "C" int kmc_version(void) { return 200; }

@@ -67,11 +67,17 @@ constexpr int kWaves4 = kCountBlock / 64;
 constexpr int kStage = 320;                  // K4 per-wave keys staged for one probe loop
 constexpr int kClaimW = 320;                 // K4 per-wave claims per pass (2-byte slot ids)
 constexpr uint32_t kMaxInitPasses = 16;
-constexpr int kPassTop = 64 - kMaxLg;          // pass bits [kPassTop - log2 P, kPassTop), below the list bits
+// K4 passes: pass_of takes the P-quantile of bits [32, kPassTop) of h times an odd
+// constant (17 bits), so a list splits into at most 2^17 passes
+constexpr int kPassTop = 64 - kMaxLg;
 constexpr uint32_t kMaxPasses = 1u << (kPassTop - 32);
 constexpr int kPassDistinct = 2048;          // keys per K4 pass aimed at (table load <= 0.47)
 constexpr int kRes = 16;                     // K4 keys per thread held in registers
 constexpr int64_t kResKeys = (int64_t)kRes * kCountBlock;
+// Bits of the call's error word (HParams::err), read by the host after the last kernel.
+constexpr uint32_t kErrPasses = 1u;  // a list beyond K4's pass bits (KMC_ERR_INVALID_ARG)
+constexpr uint32_t kErrBound = 2u;   // a queue count, list id, range or output offset out of its
+                                     // allocation: the access is skipped (KMC_ERR_INTERNAL)
 static_assert(kPassDistinct <= kWaves4 * kClaimW && kTableSlots < 65536 , "K4 sizes");
 
 struct HParams {
@@ -102,14 +108,17 @@ struct HParams {
     uint32_t *ndist;         // [lists] distinct keys per list
     uint64_t *dist_off;      // [lists + 1] exclusive scan of ndist
     int64_t lists;
-    uint32_t *err;           // set when a list exceeds what K4 can split
+    uint64_t win_cap;        // entries of ent / pk (the call's windows) and, in direct mode, the least
+                             // capacity of out_keys / out_counts: the bound of every queued range and copy
+    uint32_t *err;           // kErrPasses: a list exceeds what K4 can split; kErrBound: a bound guard fired
     uint32_t claim_cap;      // K4 claims per wave and pass (kClaimW; smaller only in tests)
     uint32_t sort_cap;       // K4s takes lists of at most this many keys (kSortCap; 0 in tests: none)
     uint32_t sort_cap_big;   // the big K4s instance takes the longer ones up to this (kSortCapBig; 0: none)
     uint64_t *big;           // [lists][3] (list, begin, end) handed by K4s to its big instance
     unsigned long long *nbig;  // their number
-    uint64_t *defer;         // [lists][3] (list, begin, end) left to the table kernel by K4s
-    unsigned long long *ndefer;  // their number
+    uint64_t *defer;         // [lists][3] (list, begin, end) for the table kernel: without direct output
+    unsigned long long *ndefer;  // the lists either K4s instance hands back; with it, only the lists longer
+                                 // than the big instance's cap (canon_classify_kernel; the first launch)
     uint64_t *rec_off;       // [n + 1] output offsets
     uint64_t *out_keys;
     uint32_t *out_counts;
@@ -126,11 +135,20 @@ struct HParams {
     unsigned long long *nfq;      // their number
     uint64_t *tq;                 // the queue this canon_table_kernel launch drains (defer or defer2)
     unsigned long long *ntq;
-    uint64_t *defer2;             // [lists][3] direct mode: the common instance's deferrals (the table
-    unsigned long long *ndefer2;  // kernel's second launch); defer holds the long lists and the big
-                                  // instance's deferrals (its first launch)
+    uint64_t *defer2;             // [lists][3] direct mode: the lists either K4s instance hands back (too
+    unsigned long long *ndefer2;  // many crowded slots), drained by the table kernel's second launch
     int64_t l_lo, l_hi;           // direct mode: the lists of this launch of the common instance
 };
+
+// Raises bit `b` of the call's error word (any thread; the host reads it after the
+// last kernel).  Round 6: every queue count, queued list id / key range, record id
+// and output offset that a kernel takes from the workspace is checked against its
+// allocation before it is used, and a value outside it raises kErrBound and skips
+// the access (the call returns KMC_ERR_INTERNAL) instead of faulting the queue
+// (section 4.4 of DESIGN.md, "The round-5 memory-aperture fault").
+__device__ __forceinline__ void raise_err(const HParams &p, uint32_t b) {
+    __hip_atomic_fetch_or(p.err, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Partition value of a key: K1 / K3a / K3b bucket and list by its top bits.  A
 // multiplicative hash (one 64-bit multiply, invertible) in the two input walks;
@@ -751,6 +769,11 @@ __device__ __forceinline__ void chain_from(const HParams &p, int64_t r, unsigned
 // offset in the record and sets *F to the record's start, or kUnknown.
 __device__ __forceinline__ unsigned long long reserve_pairs(const HParams &p, int64_t r, uint32_t cnt,
                                                             unsigned long long *F) {
+    if ((uint64_t)r >= (uint64_t)p.n) {  // (guard) not a record of this call
+        raise_err(p, kErrBound);
+        *F = kUnknown;
+        return 0;
+    }
     const unsigned long long old = __hip_atomic_fetch_add(&p.rstate[r], (unsigned long long)cnt + (1ull << kPairsBits),
                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long f = ld_agent(&p.rbase[r]);  // (issued before the add returned: independent)
@@ -767,6 +790,10 @@ __device__ __forceinline__ unsigned long long reserve_pairs(const HParams &p, in
 __device__ __forceinline__ void queue_copy(const HParams &p, uint64_t src, int64_t r, uint64_t c, uint64_t cnt) {
     if (cnt == 0) return;
     const unsigned long long i = atomicAdd(p.nfq, 1ull);
+    if (i >= 2ull * (uint64_t)p.lists) {  // (guard) at most two copies per list
+        raise_err(p, kErrBound);
+        return;
+    }
     p.fq[4 * i] = src;
     p.fq[4 * i + 1] = (uint64_t)r;
     p.fq[4 * i + 2] = c;
@@ -919,6 +946,10 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
     // more often than its dedup takes
     const int64_t G = gridDim.x, nl = (int64_t)*p.ntq;
     const uint64_t *dl = p.tq;  // (list, begin, end) triples (defer, or in direct mode defer2)
+    if ((uint64_t)nl > (uint64_t)p.lists) {  // (guard) the queue holds at most one entry per list
+        if (blockIdx.x == 0 && tid == 0) raise_err(p, kErrBound);
+        return;
+    }
     int64_t i = blockIdx.x;
     if (i >= nl) return;
     // list bounds two lists ahead, keys one list ahead
@@ -935,6 +966,16 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
         if (i + 2 * G < nl) {
             b2 = dl[3 * (i + 2 * G) + 1];
             e2 = dl[3 * (i + 2 * G) + 2];
+        }
+        // (guard, workgroup-uniform: every thread read the same triple) a list id
+        // and key range inside the call's lists and entries
+        if ((uint64_t)l >= (uint64_t)p.lists || b0 > e0 || e0 > p.win_cap) {
+            if (tid == 0) raise_err(p, kErrBound);
+            b0 = b1;
+            e0 = e1;
+            b1 = b2;
+            e1 = e2;
+            continue;
         }
         if (e0 - b0 <= (uint64_t)kResKeys) load_keys(p.ent, b0, e0, kr);
         const uint64_t n = e0 - b0;
@@ -969,7 +1010,7 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 lds_barrier();
                 par ^= 1;
                 if (P >= kMaxPasses) {  // > 2^17 x 2 560 distinct keys in one list: out of pass bits
-                    if (tid == 0) *p.err = 1u;
+                    if (tid == 0) raise_err(p, kErrPasses);
                     break;
                 }
                 P <<= 1;
@@ -983,7 +1024,10 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 before += w2 < wv ? v : 0u;
                 total += v;
             }
-            // the wave's claimed slots, in claim order (coalesced), cleared
+            // the wave's claimed slots, in claim order (coalesced), cleared; the
+            // pass's pairs stay inside the list's segment (guard: distinct <= keys)
+            const bool fits = out + total <= e0;
+            if (!fits && tid == 0) raise_err(p, kErrBound);
             const uint16_t *cl = L.cl[wv];
             for (uint32_t i = lane; i < ncl; i += 64) {
                 const uint32_t sl = cl[i];
@@ -991,7 +1035,7 @@ __global__ __launch_bounds__(kCountBlock) __attribute__((amdgpu_waves_per_eu(4))
                 const uint32_t c = L.tc[sl];
                 L.tk[sl] = kEmptyH;
                 L.tc[sl] = 0u;
-                {
+                if (fits) {
                     // keys use at most 62 bits (k <= 31): occurrences 1..3 ride in the
                     // top two bits, larger counts escape to pc (K5 reads it only then)
                     const unsigned long long tag = c < 3u ? c : 3u;
@@ -1082,15 +1126,21 @@ struct K4sLds {
 static_assert(sizeof(K4sLds<SortBig>) <= 160 * 1024, "big K4s instance: one workgroup per CU");
 static_assert(sizeof(K4sLds<SortSmall>) <= 80 * 1024, "common K4s instance: two workgroups per CU");
 
-// a list left to another kernel: its id and key range, appended to (q, nq)
-__device__ __forceinline__ void queue_list(uint64_t *q, unsigned long long *nq, int64_t l, uint64_t b, uint64_t e) {
+// a list left to another kernel: its id and key range, appended to (q, nq), a
+// queue of p.lists entries (each list is queued at most once)
+__device__ __forceinline__ void queue_list(const HParams &p, uint64_t *q, unsigned long long *nq, int64_t l,
+                                           uint64_t b, uint64_t e) {
     const unsigned long long i = atomicAdd(nq, 1ull);
+    if (i >= (uint64_t)p.lists) {  // (guard)
+        raise_err(p, kErrBound);
+        return;
+    }
     q[3 * i] = (uint64_t)l;
     q[3 * i + 1] = b;
     q[3 * i + 2] = e;
 }
 __device__ __forceinline__ void defer_list(const HParams &p, int64_t l, uint64_t b, uint64_t e) {
-    queue_list(p.defer, p.ndefer, l, b, e);
+    queue_list(p, p.defer, p.ndefer, l, b, e);
 }
 
 // The pair format (K4s, K4 -> K5): a canonical key of k <= 31 bases uses at most
@@ -1252,7 +1302,7 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         if (tid == 0) {
             // (direct output: to the table kernel's second launch, after every other
             // list; its first takes the lists too long for the big instance)
-            if (DIRECT) queue_list(p.defer2, p.ndefer2, l, b0, e0);
+            if (DIRECT) queue_list(p, p.defer2, p.ndefer2, l, b0, e0);
             else defer_list(p, l, b0, e0);
         }
         return;  // (the next list's barrier A orders the LDS reuse)
@@ -1402,7 +1452,11 @@ __device__ __forceinline__ void sort_list(const HParams &p, K4sLds<C> &S, int64_
         if (tid == 0) {
             unsigned long long F;
             const unsigned long long c = reserve_pairs(p, rec, D, &F);
-            const bool fin = F != kUnknown;
+            bool fin = F != kUnknown;
+            if (fin && F + c + D > p.win_cap) {  // (guard) past the caller's arrays: not written there
+                raise_err(p, kErrBound);
+                fin = false;
+            }
             S.mode = fin ? 1u : 0u;
             S.gbase = fin ? F + c : b0;
             if (!fin) queue_copy(p, b0, rec, c, D);  // the whole list from pk
@@ -1464,7 +1518,7 @@ __global__ __launch_bounds__(SortSmall::kBlock) __attribute__((amdgpu_waves_per_
         const uint64_t *nxt = l + gridDim.x < l_hi ? p.list_start + l + gridDim.x : nullptr;
         if (n > p.sort_cap) {  // workgroup-uniform
             if (!DIRECT && threadIdx.x == 0) {
-                if (n <= p.sort_cap_big) queue_list(p.big, p.nbig, l, b0, e0);
+                if (n <= p.sort_cap_big) queue_list(p, p.big, p.nbig, l, b0, e0);
                 else defer_list(p, l, b0, e0);
             }
             if (nxt) {
@@ -1490,6 +1544,10 @@ __global__ __launch_bounds__(SortBig::kBlock) void canon_sort_big_kernel(HParams
     // DIRECT: one group of records per launch, its segment of the (list-ordered) queue
     const int64_t q_lo = DIRECT ? (int64_t)p.dist_off[p.l_lo] : 0;
     const int64_t nl = DIRECT ? (int64_t)p.dist_off[p.l_hi] : (int64_t)*p.nbig;
+    if ((uint64_t)nl > (uint64_t)p.lists || q_lo > nl) {  // (guard)
+        if (blockIdx.x == 0 && threadIdx.x == 0) raise_err(p, kErrBound);
+        return;
+    }
     for (int64_t i = q_lo + blockIdx.x; i < nl; i += gridDim.x) {
         const uint64_t b0 = p.big[3 * i + 1], e0 = p.big[3 * i + 2];
         const int64_t in = i + gridDim.x;
@@ -1602,10 +1660,19 @@ __global__ __launch_bounds__(1024) void canon_direct_final_kernel(HParams p) {
 // Direct output: the pairs left in pk (lists whose record start was not yet known,
 // or that the table kernel counted) to their place; one workgroup per queue entry.
 __global__ __launch_bounds__(256) void canon_fallback_kernel(HParams p) {
-    const int64_t nq = (int64_t)*p.nfq;
+    int64_t nq = (int64_t)*p.nfq;
+    if ((uint64_t)nq > 2ull * (uint64_t)p.lists) {  // (guard) queue_copy stops there
+        if (blockIdx.x == 0 && threadIdx.x == 0) raise_err(p, kErrBound);
+        nq = 2 * p.lists;
+    }
     for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
-        const uint64_t src = p.fq[4 * q], c = p.fq[4 * q + 2], m = p.fq[4 * q + 3];
-        const uint64_t dst = p.rbase[p.fq[4 * q + 1]] + c;
+        const uint64_t src = p.fq[4 * q], r = p.fq[4 * q + 1], c = p.fq[4 * q + 2], m = p.fq[4 * q + 3];
+        // (guard, workgroup-uniform) a record of the call, source and target inside their arrays
+        const uint64_t dst = r < (uint64_t)p.n ? p.rbase[r] + c : ~0ull;
+        if (r >= (uint64_t)p.n || src > p.win_cap || m > p.win_cap - src || dst > p.win_cap || m > p.win_cap - dst) {
+            if (threadIdx.x == 0) raise_err(p, kErrBound);
+            continue;
+        }
         for (uint64_t i = threadIdx.x; i < m; i += 256) {
             const unsigned long long x = p.pk[src + i];
             const uint32_t tag = (uint32_t)(x >> 62);
@@ -1634,6 +1701,10 @@ constexpr int64_t kGroupLists = 8192;  // direct output: lists per launch of the
 unsigned long long h_fb_entries = 0, h_fb_pairs = 0;
 std::vector<unsigned long long> h_fb_rec;  // fallback pairs per record
 unsigned long long h_fb_defer[3] = {0, 0, 0};  // lists queued: big instance, table (long / big's), table (common's)
+// kmc_diag_canon_stale_queue: >= 0 -> the table kernel's second queue count starts the
+// call at this value instead of 0 (a counter left un-reset: entries it covers were
+// never written by this call); -1: off
+long long h_stale_queue = -1;
 #endif
 
 inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -1711,6 +1782,18 @@ extern "C" KMC_DIAG_API int kmc_diag_canon_fallback_detail(unsigned long long *p
     std::lock_guard<std::mutex> lk(h_mu);
     for (unsigned i = 0; i < cap && i < h_fb_rec.size(); ++i) per_rec[i] = h_fb_rec[i];
     for (int j = 0; j < 3; ++j) queued3[j] = h_fb_defer[j];
+    return KMC_OK;
+}
+
+// Test hook (diagnostic library only, not in kmc.h): the defect class behind the
+// round-5 fault -- a queue counter that a call does not reset,
+// so that the table kernel's second launch takes entries this call never wrote
+// (in a reused or caller workspace: stale or arbitrary bytes).  v >= 0: the count
+// of defer2 starts at v; -1 restores the reset.  With the bound guards the call
+// returns KMC_ERR_INTERNAL instead of faulting.
+extern "C" KMC_DIAG_API int kmc_diag_canon_stale_queue(long long v) {
+    std::lock_guard<std::mutex> lk(h_mu);
+    h_stale_queue = v < 0 ? -1 : v;
     return KMC_OK;
 }
 
@@ -1895,6 +1978,7 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     p.cpw = P.cpw;
     const int64_t M = P.M, Mc = P.Mc, L = P.L;
     p.lists = L;
+    p.win_cap = (uint64_t)P.windows;
     const int64_t NF = (int64_t)P.fsplit.size();
     const size_t total = P.total;
     const size_t o_idx = P.o_idx, o_lg = P.o_lg, o_cb = P.o_cb, o_ccb = P.o_ccb, o_w0 = P.o_w0, o_nw = P.o_nw,
@@ -1990,6 +2074,16 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
     if ((he = hipMemsetAsync(p.err, 0, 4, stream)) || (he = hipMemsetAsync(p.ndefer, 0, 8, stream)) ||
         (he = hipMemsetAsync(p.nbig, 0, 8, stream)) || (he = hipMemsetAsync(p.ndefer2, 0, 8, stream)))
         return (int)he;
+#ifdef KMC_DIAG_HOOKS
+    {
+        static unsigned long long stale;  // (static: the async copy reads it after this frame)
+        std::lock_guard<std::mutex> lk(h_mu);
+        if (h_stale_queue >= 0) {
+            stale = (unsigned long long)h_stale_queue;
+            if ((he = hipMemcpyAsync(p.ndefer2, &stale, 8, hipMemcpyHostToDevice, stream))) return (int)he;
+        }
+    }
+#endif
     if (direct)
         hipLaunchKernelGGL(canon_direct_setup_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, stream, p);
     if (M > 0) {
@@ -2041,7 +2135,7 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
             hipLaunchKernelGGL(canon_sort_kernel<true>, gg, dim3(kSortBlock), 0, stream, pg);
             r0 = r1;
         }
-        HParams p2 = p;  // the common instance's deferrals
+        HParams p2 = p;  // the lists both K4s instances handed back (defer2)
         p2.tq = p.defer2;
         p2.ntq = p.ndefer2;
         hipLaunchKernelGGL(canon_table_kernel, g_table, dim3(kCountBlock), 0, stream, p2);
@@ -2055,6 +2149,7 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
             (he = hipMemcpyAsync(&err, p.err, 4, hipMemcpyDeviceToHost, stream)) ||
             (he = hipStreamSynchronize(stream)))
             return (int)he;
+        if (err & kErrBound) return KMC_ERR_INTERNAL;
         if (err) return KMC_ERR_INVALID_ARG;  // a record far beyond any genome (see kMaxPasses)
         *num_distinct = distinct;
 #ifdef KMC_DIAG_HOOKS
@@ -2097,6 +2192,7 @@ extern "C" int kmc_count_canonical_hash_ex(const char *data, const int64_t *indi
         (he = hipMemcpyAsync(&distinct, p.dist_off + L, 8, hipMemcpyDeviceToHost, stream)) ||
         (he = hipMemcpyAsync(&err, p.err, 4, hipMemcpyDeviceToHost, stream)) || (he = hipStreamSynchronize(stream)))
         return (int)he;
+    if (err & kErrBound) return KMC_ERR_INTERNAL;
     if (err) return KMC_ERR_INVALID_ARG;  // a record far beyond any genome (see kMaxPasses)
     *num_distinct = distinct;
     if (distinct > capacity) return KMC_ERR_CAPACITY;

@@ -230,6 +230,14 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     if (!data || !indices || !sum || ndev < 1) return KMC_ERR_INVALID_ARG;
     if (k < 1 || k > KMC_DENSE_MAX_K) return KMC_ERR_UNSUPPORTED_K;
     if ((uint64_t)indices[num_seqs] > data_bytes) return KMC_ERR_INVALID_ARG;
+    // int32 counts of a record of 2^31 or more windows could wrap in the all-reduce:
+    // each shard sees fewer than 2^31 of its windows (so no shard's device check
+    // fires), but their int32 sum is the whole record's.  The offsets are on the
+    // host here, so every record is checked before anything is planned.
+    for (uint64_t s = 0; s < num_seqs; ++s) {
+        if (indices[s + 1] < indices[s]) return KMC_ERR_INVALID_ARG;
+        if (indices[s + 1] - indices[s] - k >= ((int64_t)1 << 31)) return KMC_ERR_RECORD_TOO_LONG;
+    }
     int visible = 0;
     if (hipGetDeviceCount(&visible) != hipSuccess || visible < 1) return KMC_ERR_NO_DEVICE;
     std::vector<int> devs(ndev);
@@ -292,33 +300,43 @@ extern "C" int kmc_count_multi(const char *data, const int64_t *indices, uint64_
     if (nr == ncclSuccess) nr = ncclGroupEnd();
     else ncclGroupEnd();
     bool comm_ok = nr == ncclSuccess;
+    // a HIP failure after the collective (a stream or copy error) is reported as its
+    // hipError_t, not as an RCCL failure: no RCCL call failed
+    hipError_t he = hipSuccess;
     if (comm_ok) {
         for (auto *d : b) {  // the collective itself finished on every device
             (void)hipSetDevice(d->dev);
-            if (hipStreamSynchronize(d->st) != hipSuccess) comm_ok = false;
+            const hipError_t e = hipStreamSynchronize(d->st);
+            if (e != hipSuccess && he == hipSuccess) he = e;
         }
-        if (!comm_ok) nr = ncclSystemError;
+        // (a stream that failed to drain may hold a collective in an error state)
+        if (he != hipSuccess) comm_ok = false;
     }
     int st = KMC_OK;  // every device has synchronised: the shards' own status words
-    if (nr == ncclSuccess)
+    if (nr == ncclSuccess && he == hipSuccess)
         for (auto *d : b) {
             int32_t v = 0;
             (void)hipSetDevice(d->dev);
-            if (hipMemcpy(&v, d->status, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) nr = ncclSystemError;
-            else if (v != KMC_OK && st == KMC_OK) st = v;
+            const hipError_t e = hipMemcpy(&v, d->status, sizeof(v), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                if (he == hipSuccess) he = e;
+            } else if (v != KMC_OK && st == KMC_OK) {
+                st = v;
+            }
         }
-    if (nr == ncclSuccess) {
+    if (nr == ncclSuccess && he == hipSuccess) {
         DevState &d = *b[0];
         (void)hipSetDevice(d.dev);
-        if (hipMemcpyAsync(sum, d.sum, sum_bytes, hipMemcpyDeviceToHost, d.st) != hipSuccess) nr = ncclSystemError;
-        if (invalid &&
-            hipMemcpyAsync(invalid, d.inv, num_seqs * sizeof(int32_t), hipMemcpyDeviceToHost, d.st) != hipSuccess)
-            nr = ncclSystemError;
-        if (hipStreamSynchronize(d.st) != hipSuccess) nr = ncclSystemError;
+        he = hipMemcpyAsync(sum, d.sum, sum_bytes, hipMemcpyDeviceToHost, d.st);
+        if (he == hipSuccess && invalid)
+            he = hipMemcpyAsync(invalid, d.inv, num_seqs * sizeof(int32_t), hipMemcpyDeviceToHost, d.st);
+        const hipError_t e = hipStreamSynchronize(d.st);
+        if (he == hipSuccess) he = e;
     }
     if (!comm_ok) drop_comms(devs);
     (void)hipSetDevice(cur);
     if (nr != ncclSuccess) return KMC_ERR_RCCL;
+    if (he != hipSuccess) return (int)he;
     return st;
 }
 

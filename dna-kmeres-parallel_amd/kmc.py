@@ -32,6 +32,7 @@ MAX_SEQS_REFERENCE = 100
 DROPIN_K = 3
 KMC_ERR_CAPACITY = 1009
 KMC_ERR_RECORD_TOO_LONG = 1010
+KMC_ERR_INTERNAL = 1011
 
 
 class KmcError(RuntimeError):
@@ -89,6 +90,7 @@ class diag:
             _diag_lib.kmc_diag_canon_fallback_detail.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_uint,
                                                                  ctypes.POINTER(ctypes.c_ulonglong)]
             _diag_lib.kmc_diag_dense_spill_cap.argtypes = [ctypes.c_uint]
+            _diag_lib.kmc_diag_canon_stale_queue.argtypes = [ctypes.c_longlong]
         self._prev = _active
         _active = _diag_lib
         return _diag_lib
@@ -102,6 +104,7 @@ class diag:
         L.kmc_diag_canon_sort_cap(1 << 30)  # (also restores the big instance's cap)
         L.kmc_diag_canon_direct(1)
         L.kmc_diag_dense_spill_cap(0)
+        L.kmc_diag_canon_stale_queue(-1)
         _active = self._prev
         return False
 
@@ -122,15 +125,19 @@ def _load(path):
     own.  A second runtime mapped anyway is refused here."""
     if not os.path.exists(path):
         raise RuntimeError("%s not built: run `make -C %s` (no CPU fallback exists)" % (os.path.basename(path), HERE))
-    try:
-        import torch  # noqa: F401  (maps torch's HIP runtime before libkmc's NEEDED entry is resolved)
-    except ImportError:
-        pass
+    # KMC_NO_TORCH=1: host-only use of the binding (loader, shard planner) without
+    # paying torch's import; such a process must then not import torch at all
+    if os.environ.get("KMC_NO_TORCH") != "1":
+        try:
+            import torch  # noqa: F401  (maps torch's HIP runtime before libkmc's NEEDED entry is resolved)
+        except ImportError:
+            pass
     L = ctypes.CDLL(path)
     rt = hip_runtimes()
     if len(rt) > 1:
-        raise RuntimeError("two HIP runtimes are mapped in this process (%s): load %s after importing torch, "
-                           "not before" % (", ".join(rt), os.path.basename(path)))
+        raise RuntimeError("two HIP runtimes are mapped in this process (%s): each would initialise the GPU on its "
+                           "own, so %s is refused; import torch before loading it (or set KMC_NO_TORCH=1 only in "
+                           "processes that never import torch)" % (", ".join(rt), os.path.basename(path)))
     L.kmc_error_string.restype = ctypes.c_char_p
     L.kmc_error_string.argtypes = [ctypes.c_int]
     L.kmc_version.restype = ctypes.c_int

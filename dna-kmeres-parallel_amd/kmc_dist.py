@@ -43,10 +43,20 @@ def gpu_counter(device):
     return count
 
 
+def check_record_windows(indices, k):
+    """Raise KmcError(KMC_ERR_RECORD_TOO_LONG) when a record has 2^31 or more
+    windows: every shard of it has fewer (no rank's device check fires), but the
+    all_reduce adds the int32 parts of the whole record, which could wrap."""
+    idx = np.asarray(indices, dtype=np.int64)
+    if idx.size > 1 and int((np.diff(idx) - k).max()) >= 1 << 31:
+        raise kmc.KmcError(kmc.KMC_ERR_RECORD_TOO_LONG, "count_sharded")
+
+
 def count_sharded(data, indices, k, counter, group=None):
     """Histogram of the whole buffer, computed by this rank's shard + all_reduce."""
     import torch.distributed as dist
 
+    check_record_windows(indices, k)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     shard = kmc.plan_shards(indices, k, world)[rank]

@@ -65,13 +65,19 @@ enum kmc_status {
     KMC_ERR_RCCL = 1007,          /* RCCL call failed */
     KMC_ERR_NO_DEVICE = 1008,     /* no HIP device visible */
     KMC_ERR_CAPACITY = 1009,      /* caller output smaller than the result (size reported) */
-    KMC_ERR_RECORD_TOO_LONG = 1010 /* a record has >= 2^31 windows in one dense call: int32 counts could wrap */
+    KMC_ERR_RECORD_TOO_LONG = 1010, /* a record has >= 2^31 windows in one dense call: int32 counts could wrap */
+    KMC_ERR_INTERNAL = 1011         /* a device-side bound check fired (a library defect): the access was
+                                       skipped and the call's outputs are not valid (kmc_count_canonical_hash) */
 };
 
 /* Human-readable text for a kmc_status or hipError_t code (static storage). */
 KMC_API const char *kmc_error_string(int code);
 
-/* Library version: major*10000 + minor*100 + patch. */
+/* Library version: major*10000 + minor*100 + patch.  200 (0.2.0): kmc_dense_args
+ * ends with `status` (below) and KMC_ERR_INTERNAL exists; a caller built against
+ * an older header (0.1.0, a shorter kmc_dense_args) must not call
+ * kmc_count_dense_ex on this library -- check kmc_version() >= 200 first. */
+#define KMC_VERSION 200
 KMC_API int kmc_version(void);
 
 /* ------------------------------------------------------------------------ */
@@ -192,7 +198,11 @@ KMC_API int kmc_plan_shards(const int64_t *indices, uint64_t num_seqs, int k, in
  * take turns (RCCL communicators are not reentrant), calls on disjoint sets run
  * concurrently, and a set whose collective failed is rebuilt by the next call.
  * Each shard's count carries its own status word: KMC_ERR_CAPACITY /
- * KMC_ERR_RECORD_TOO_LONG (kmc_count_dense_ex) are returned by this call.
+ * KMC_ERR_RECORD_TOO_LONG (kmc_count_dense_ex) are returned by this call.  A record
+ * of 2^31 or more windows is refused up front (KMC_ERR_RECORD_TOO_LONG, checked on
+ * the host offsets before any device work): its shards would each hold fewer, but
+ * the all-reduce would add their int32 parts.  HIP failures after the all-reduce
+ * return their hipError_t; KMC_ERR_RCCL only when an RCCL call failed.
  * Retention: the cached per-device buffers are sized to the largest shard + halo
  * seen (GBs per device for Gbase inputs) plus 64 MB of pinned staging, and are
  * held until kmc_multi_release().  kmc_set_reserved_cus does not apply here (the

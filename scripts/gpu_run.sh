@@ -8,6 +8,8 @@
 #          profile        scripts/profile_bench.sh: kernel trace + HBM and LDS PMC passes
 #          cbench[:CFGS]  scripts/cbench.py --configs CFGS (default c1,c3,c4,c4r) under the kernel trace
 #          shard          scripts/shardbench.py (one rank's step of an N-way job, N = 1, 2, 4, 8)
+#          pmcshards      scripts/pmc_shards.py run under the FETCH_SIZE and WRITE_SIZE passes (then
+#                         `pmc_shards.py parse` here -> profiles/pmc_dense_k8_shards.json)
 #          fuzz           the dense and canonical fuzzers
 # Every step has its own time limit; the first failing step ends the call.
 # Output: gpurun_out/TAG/<step>.log (+ rocprofv3 directories).
@@ -34,6 +36,10 @@ for s in "$@"; do
         cbench:*) run 900 $O/cbench.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/cbench_prof -o cb \
                       -- python3 scripts/cbench.py --iters 3 --configs "${s#cbench:}" ;;
         shard) run 600 $O/shard.log python scripts/shardbench.py ;;
+        pmcshards) run 600 $O/pmc_fetch.log rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_128B --output-format csv \
+                       -d $O/pmc_fetch -o ps -- python3 scripts/pmc_shards.py run &&
+                   run 600 $O/pmc_write.log rocprofv3 --pmc WRITE_SIZE --output-format csv \
+                       -d $O/pmc_write -o ps -- python3 scripts/pmc_shards.py run ;;
         fuzz) run 600 $O/fuzz_dense.log python scripts/fuzz_dense.py && run 600 $O/fuzz_canonical.log python scripts/fuzz_canonical.py ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -29,6 +29,8 @@ def run():
     import bench
     import kmc
     dev = torch.device("cuda:0")
+    # the build measured (bench.py reports a PMC entry only for the same build)
+    print(json.dumps({"build_id": bench.dense_code_object_id(kmc.LIB_PATH)}), flush=True)
     k, L = 8, 1_000_000_000
     nb = 1 << (2 * k)
     for world in (1, 2, 4, 8):
@@ -69,7 +71,9 @@ def per_dispatch(d):
 
 
 def parse(fetch_dir, write_dir, log, dst):
-    shards = [json.loads(l) for l in open(log) if l.startswith("{")]
+    lines = [json.loads(l) for l in open(log) if l.startswith("{")]
+    build_id = next(x["build_id"] for x in lines if "build_id" in x)
+    shards = [x for x in lines if "world" in x]
     f, w = per_dispatch(fetch_dir), per_dispatch(write_dir)
     assert len(f["FETCH_SIZE"]) == LAUNCHES * len(shards) == len(w["WRITE_SIZE"]), \
         (len(f["FETCH_SIZE"]), len(w["WRITE_SIZE"]), len(shards))
@@ -79,7 +83,7 @@ def parse(fetch_dir, write_dir, log, dst):
         mean = lambda xs: sum(xs[sl]) / len(xs[sl])
         fetch_kib, write_kib = mean(f["FETCH_SIZE"]), mean(w["WRITE_SIZE"])
         e = {"k": 8, "data_bytes": s["data_bytes"], "shard": "world %d rank %d" % (s["world"], s["rank"]),
-             "kernel": KERNEL, "fetch_size_kib_per_launch": fetch_kib, "write_size_kib_per_launch": write_kib,
+             "kernel": KERNEL, "build_id": build_id, "fetch_size_kib_per_launch": fetch_kib, "write_size_kib_per_launch": write_kib,
              "hbm_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024,
              "correction": "gfx950: FETCH_SIZE counts a 128-B read request as 64 B (x2; MI355X_MICROARCH.md "
                            "HBM section), cross-checked by TCC_EA0_RDREQ_128B x 128 B",

@@ -58,6 +58,8 @@ def lds_summary(line, k, kern, cus=256, xcds=8, last=10):
         # the binding roof: the share of the kernel's cycles in which an average CU's
         # LDS array is busy (1.0 = the kernel runs at the LDS floor)
         "lds_busy_frac": a / cus / cyc,
+        # the build measured: the bench line's code-object id of count_dense_kernel
+        "build_id": line.get("roofline", {}).get("build_id"),
         "source": "rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS_ATOMIC GRBM_GUI_ACTIVE of "
                   "python3 bench.py --steps 20 --warmup 14 (scripts/profile_bench.sh), the last %d full-size "
                   "launches; kernel cycles = GRBM_GUI_ACTIVE / 8 XCDs (MI355X_MICROARCH.md DVFS note); "
@@ -115,6 +117,7 @@ def main():
             "correction": "gfx950: FETCH_SIZE counts a 128-B read request as 64 B (x2; MI355X_MICROARCH.md HBM "
                           "section), confirmed here by TCC_EA0_RDREQ_128B x 128 B",
             "launches_sampled": [len(fetch), len(write)],
+            "build_id": line.get("roofline", {}).get("build_id"),
             "source": "rocprofv3 --pmc FETCH_SIZE TCC_EA0_RDREQ_128B TCC_EA0_RDREQ_64B / --pmc WRITE_SIZE "
                       "(separate passes) of python3 bench.py --steps 3",
         }

@@ -39,7 +39,8 @@ def test_diag_library_adds_only_the_test_hooks(kmc):
     assert hooks == ["kmc_diag_canon_claim_cap", "kmc_diag_canon_direct", "kmc_diag_canon_fallback",
                      "kmc_diag_canon_fallback_detail",
                      "kmc_diag_canon_sort_cap",
-                     "kmc_diag_canon_sort_cap_big", "kmc_diag_dense_spill_cap", "kmc_diag_radix_mode"]
+                     "kmc_diag_canon_sort_cap_big", "kmc_diag_canon_stale_queue", "kmc_diag_dense_spill_cap",
+                     "kmc_diag_radix_mode"]
     assert sorted(set(got) - set(hooks)) == kmc.header_symbols()
     assert kmc.lib() is not None
     with kmc.diag() as D:  # inside diag() every binding uses the diagnostic library
@@ -51,7 +52,9 @@ def test_diag_library_adds_only_the_test_hooks(kmc):
 def test_error_strings_and_version(kmc):
     assert kmc.error_string(0) == "success"
     assert "aligned" in kmc.error_string(1003)
-    assert kmc.lib().kmc_version() >= 100
+    # 0.2.0: kmc_dense_args carries `status` (the ctypes mirror must match it)
+    assert kmc.lib().kmc_version() == 200
+    assert [f[0] for f in kmc.DenseArgs._fields_][-1] == "status"
 
 
 def test_argument_errors_need_no_device(kmc):

@@ -286,8 +286,9 @@ def _finalize_worker(rank, world, port, q):
     win = plan["win"]
     alg = (win[1] - win[0]) + 4 * (1 << (2 * k)) * records
     kern_ms = 0.5 + rank  # rank 1 is the slow one
+    steps = [kern_ms + 0.1 * i for i in range(5)]  # per-step kernel times: median kern_ms + 0.2
     res = bench.finalize(args, world, rank, "gloo", data, matrix, L, k, records, win, 0.01 * (1 + rank), kern_ms,
-                         alg, timer="host")
+                         alg, timer="host", step_ms=steps)
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -301,6 +302,9 @@ def test_gloo_world2_bench_line_fields():
     # max over ranks: rank 1's elapsed and kernel time
     assert abs(r["ms_per_step"] - 0.02 / 5 * 1e3) < 1e-9 and r["roofline"]["kernel_ms"] == 1.5
     rf = r["roofline"]
+    # per-step spread of the slowest rank (rank 1: 1.5 .. 1.9 ms)
+    assert abs(rf["kernel_ms_median"] - 1.7) < 1e-9 and rf["kernel_ms_min"] == 1.5 and abs(rf["kernel_ms_max"] - 1.9) < 1e-9
+    assert rf["build_id"] is None and rf["traffic"] is None  # host timer: no GPU build measured
     for key in ("achieved", "frac", "node_achieved", "node_frac", "node_peak", "alg_bytes_per_kmer"):
         assert rf[key] > 0, key
     assert rf["node_peak"] == 2 * rf["peak"]
@@ -309,3 +313,51 @@ def test_gloo_world2_bench_line_fields():
     assert r["allreduce"]["ms"] > 0 and r["allreduce"]["bytes"] == 4 * 65536 * 4
     cb = r["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] in ("reference", "port")
+
+
+def test_multi_refuses_a_record_of_2p31_windows_on_the_host(kmc):
+    """kmc_count_multi splits records over devices, so no shard's own device check
+    sees 2^31 windows of one record; the host offsets are checked first
+    (KMC_ERR_RECORD_TOO_LONG) before any HIP call.  A record of 2^31 - 1 windows
+    passes that check (and then needs a device: not RECORD_TOO_LONG)."""
+    import ctypes
+    L = kmc.lib()
+    buf = (ctypes.c_char * 64)()
+    out = (ctypes.c_int32 * 16)()
+    for k, extra, too_long in ((3, 0, True), (3, -1, False), (8, 0, True), (1, 5, True)):
+        idx = np.array([0, 10, 10 + (1 << 31) + k + extra], dtype=np.int64)
+        rc = L.kmc_count_multi(ctypes.cast(buf, ctypes.c_void_p), idx.ctypes.data_as(ctypes.c_void_p), 2,
+                               int(idx[-1]), k, 1, None, ctypes.cast(out, ctypes.c_void_p), None)
+        assert (rc == kmc.KMC_ERR_RECORD_TOO_LONG) == too_long, (k, extra, rc)
+
+
+def test_count_sharded_refuses_a_record_of_2p31_windows():
+    """The torch.distributed path (kmc_dist.count_sharded) makes the same host check
+    before it counts or all-reduces anything."""
+    import kmc
+    import kmc_dist
+    idx = np.array([0, 100, 100 + (1 << 31) + 8], dtype=np.int64)
+    with pytest.raises(kmc.KmcError) as ei:
+        kmc_dist.count_sharded(None, idx, 8, counter=None, group=None)
+    assert ei.value.code == kmc.KMC_ERR_RECORD_TOO_LONG
+    kmc_dist.check_record_windows(idx - np.array([0, 0, 1]), 8)  # 2^31 - 1 windows: accepted
+
+
+def test_bench_pmc_entries_are_tied_to_the_build(tmp_path, kmc):
+    """bench.py reports a PMC traffic / LDS figure only from an entry taken on the
+    build it runs (the id of libkmc.so's count_dense_kernel code object): a
+    matching entry is used, an entry of another build or one without an id is not."""
+    import json
+    import bench
+    bid = bench.dense_code_object_id(kmc.LIB_PATH)
+    assert bid is not None and len(bid) == 16
+    assert bench.dense_code_object_id(kmc.DIAG_LIB_PATH) not in (None, bid)  # another build of the kernel
+    e = {"k": 8, "data_bytes": 1000, "hbm_bytes_per_launch": 1234.0}
+    p = tmp_path / "pmc.json"
+    for entry, want in ((dict(e, build_id=bid), 1234.0), (dict(e, build_id="0" * 16), None), (e, None)):
+        p.write_text(json.dumps([entry]))
+        assert bench.pmc_traffic(str(p), 8, 1000, bid) == want
+    lds = {"k": 8, "lds_busy_frac": 0.9}
+    for entry, ok in ((dict(lds, build_id=bid), True), (dict(lds, build_id="x"), False), (lds, False)):
+        p.write_text(json.dumps(entry))
+        assert (bench.lds_floor(str(p), 8, bid) is not None) == ok
