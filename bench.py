@@ -51,7 +51,7 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=14)  # the clocks settle over ~10 launches
+    ap.add_argument("--warmup", type=int, default=14)  # the clocks settle over ~10 launches (after the guard step)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: --records records in total, byte-range shards; weak: --records per GPU")
@@ -338,35 +338,36 @@ def main():
     for b, e in ev:  # materialise the events before handing them to the library
         b.record(stream)
         e.record(stream)
-    # warm-up: the correctness guard runs on an early warm result, and the last
-    # warm-up steps follow it, so that the clocks that dropped while the host
-    # checked are back up when the timed steps start (after idling, the GPU ramps
-    # its clock over ~10 launches of this kernel: profiles/r01_kernel_launches.json)
-    n_after = min(12, max(args.warmup - 1, 0))
-    last = 0
-    for i in range(args.warmup - n_after):
-        last = step(i)
+    # the correctness guard runs BEFORE the warm-up (round 6), so that the W warm-up
+    # steps run back to back right before the timed region: the host's expected
+    # slice histogram is computed first (the GPU idles then anyway), then one step
+    # (not one of the W) and the slice are counted and compared.  Until round 5 the
+    # guard ran between warm-up steps, and with the driver's --warmup 5 only four
+    # steps followed the host's check, while the clock, dropped during it, ramps over
+    # ~10 launches of this kernel (profiles/r01_kernel_launches.json): the driver's
+    # kernel time then included the ramp (BENCH_r05 2.126 ms, against 2.05-2.07 ms
+    # with 14 warm-up steps).
+    s_lo = win_lo - base
+    s_len = min(1 << 20, L - (win_lo % (L + 1)), max(win_hi - win_lo, 0))
+    exp = host_kmer_hist(kmc.synth_host_range(win_lo, win_lo + s_len, L, seed), k) if s_len >= k else None
+    last = step(0)
     drain()
     torch.cuda.synchronize()
-    if args.warmup > 0:
-        # (1) every window of the synthetic input is valid: after the all-reduce each
-        # record's column sums to L-k+1; (2) bins, not only totals: a 1 Mbase slice of
-        # this rank's bytes counted as a record of its own equals a numpy histogram of
-        # the same bytes regenerated on the host
-        tot = bufs[last].to(torch.int64).sum(dim=0)
-        if not bool((tot == (L - k + 1)).all()):
-            raise SystemExit("count check failed: column sums %s" % tot[:4].tolist())
-        s_lo = win_lo - base
-        s_len = min(1 << 20, L - (win_lo % (L + 1)), max(win_hi - win_lo, 0))
-        if s_len >= k:
-            sl = torch.zeros(s_len + 16, dtype=torch.uint8, device=dev)
-            sl[:s_len] = data[s_lo:s_lo + s_len]
-            got, _ = kmc.count_dense(sl, torch.tensor([0, s_len + 1], dtype=torch.int64, device=dev), k)
-            exp = host_kmer_hist(kmc.synth_host_range(win_lo, win_lo + s_len, L, seed), k)
-            if not np.array_equal(got.view(-1).cpu().numpy().astype(np.int64), exp):
-                raise SystemExit("count check failed: a 1 Mbase slice differs from its host histogram")
-    for i in range(args.warmup - n_after, args.warmup):
-        step(i)
+    # (1) every window of the synthetic input is valid: after the all-reduce each
+    # record's column sums to L-k+1; (2) bins, not only totals: a 1 Mbase slice of
+    # this rank's bytes counted as a record of its own equals a numpy histogram of
+    # the same bytes regenerated on the host
+    tot = bufs[last].to(torch.int64).sum(dim=0)
+    if not bool((tot == (L - k + 1)).all()):
+        raise SystemExit("count check failed: column sums %s" % tot[:4].tolist())
+    if exp is not None:
+        sl = torch.zeros(s_len + 16, dtype=torch.uint8, device=dev)
+        sl[:s_len] = data[s_lo:s_lo + s_len]
+        got, _ = kmc.count_dense(sl, torch.tensor([0, s_len + 1], dtype=torch.int64, device=dev), k)
+        if not np.array_equal(got.view(-1).cpu().numpy().astype(np.int64), exp):
+            raise SystemExit("count check failed: a 1 Mbase slice differs from its host histogram")
+    for i in range(args.warmup):
+        step(i + 1)
     drain()
 
     if world > 1:
@@ -571,8 +572,10 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
             "kernel_ms_median": k_med,
             "kernel_ms_min": k_min,
             "kernel_ms_max": k_max,
+            "kernel_ms_steps": [round(x, 4) for x in (step_ms or [])] if rank == 0 else None,
             "kernel_ms_how": "per timed step, HIP events around the histogram launch; kernel_ms is their mean "
-                             "(achieved / frac use it), median / min / max over the steps (each the slowest rank's)",
+                             "(achieved / frac use it), median / min / max over the steps (each the slowest rank's); "
+                             "kernel_ms_steps: rank 0's, in step order (a clock still ramping shows in the first)",
             "alg_bytes_per_launch": alg_bytes,
             "build_id": build_id,
             "traffic_how": ("HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE of this "

@@ -4,7 +4,9 @@
 #   steps: tests[:EXPR]   pytest -m gpu (EXPR: a -k expression)
 #          abi            the CPU ABI tests in a process of their own (no torch first)
 #          smoke          __graft_entry__.smoke()
-#          bench          python bench.py (the driver's default line)
+#          bench          python bench.py (the default line; bench5: the driver's own --warmup 5)
+#          rehearsal      bench.py --gpus 2 with gloo, both ranks on the one GPU (strong, then weak): the
+#                         N > 1 line's fields, not a measurement
 #          profile        scripts/profile_bench.sh: kernel trace + HBM and LDS PMC passes
 #          cbench[:CFGS]  scripts/cbench.py --configs CFGS (default c1,c3,c4,c4r) under the kernel trace
 #          shard          scripts/shardbench.py (one rank's step of an N-way job, N = 1, 2, 4, 8)
@@ -30,6 +32,9 @@ for s in "$@"; do
         abi) run 300 $O/abi.log $PYT tests/test_abi.py ;;
         smoke) run 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run 600 $O/bench.log python bench.py; grep '^{' $O/bench.log > $O/bench.json ;;
+        bench5) run 600 $O/bench5.log python bench.py --gpus 1 --steps 20 --warmup 5; grep '^{' $O/bench5.log > $O/bench5.json ;;
+        rehearsal) run 600 $O/rehearsal_strong.log env KMC_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 &&
+                   run 600 $O/rehearsal_weak.log env KMC_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --scaling weak --records 2 ;;
         profile) run 1100 $O/profile.log bash scripts/profile_bench.sh ;;
         cbench) run 900 $O/cbench.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/cbench_prof -o cb \
                     -- python3 scripts/cbench.py --iters 3 ;;
