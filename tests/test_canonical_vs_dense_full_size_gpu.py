@@ -17,6 +17,11 @@ kernel, direct output and the fallback copy all sit between the two.  With
 KMC_CANON_SOFTMASK the canonical call counts lowercase a/c/g/t as bases; the
 dense path counts uppercase only, so it runs on the buffer with a/c/g/t
 uppercased (the soft-mask rule of kmc.h applied to the bytes).
+
+The canonical folding itself is tied the same way (round 6): k = 13 is odd, so no
+13-mer is its own reverse complement, and the canonical count of key c (c <
+rc(c)) is dense[c] + dense[rc(c)] -- every record's canonical (non-forward) lists
+must equal that fold of the dense histogram, key for key, and list nothing else.
 """
 import os
 import sys
@@ -52,10 +57,20 @@ def uppercase_bases(data):
     return out
 
 
-def check_forward_equals_dense(kmc, data, idx, soft):
+def revcomp_msb(x, k):
+    """Key of the reverse complement of 2k-bit MSB-first keys (int64 tensor)."""
+    r = (x & 3) ^ 3
+    for q in range(1, k):
+        r = (r << 2) | (((x >> (2 * q)) & 3) ^ 3)
+    return r
+
+
+def check_against_dense(kmc, data, idx, soft, forward=True):
+    """Forward mode: each record's lists == its dense histogram (keys as LE codes).
+    Canonical mode (odd k): each record's lists == the reverse-complement fold of it."""
     import torch
     n = idx.numel() - 1
-    flags = kmc.CANON_FORWARD | (kmc.CANON_SOFTMASK if soft else 0)
+    flags = (kmc.CANON_FORWARD if forward else 0) | (kmc.CANON_SOFTMASK if soft else 0)
     keys, counts, off = kmc.count_canonical(data, idx, K, flags=flags)
     torch.cuda.synchronize()
     dense_in = uppercase_bases(data) if soft else data
@@ -65,22 +80,37 @@ def check_forward_equals_dense(kmc, data, idx, soft):
     off_h = off.cpu().tolist()
     nb = 1 << (2 * K)
     col = torch.zeros(nb, dtype=torch.int32, device=data.device)
+    if not forward:  # per MSB key: its LE bin, its reverse complement, whether it is the canonical one
+        allk = torch.arange(nb, dtype=torch.int64, device=data.device)
+        le_all = msb_to_le(allk, K)
+        rc_all = revcomp_msb(allk, K)
+        canon = allk < rc_all
+        assert not bool((allk == rc_all).any())  # odd k: no palindromes
+        del allk
     total = 0
     for s in range(n):
         a, b = off_h[s], off_h[s + 1]
         kk = keys[a:b]
         assert int((kk < 0).sum()) == 0 and int((kk >= nb).sum()) == 0, "record %d: key >= 4^k" % s
-        le = msb_to_le(kk, K)
         col.zero_()
-        col[le] = counts[a:b]
+        if forward:
+            col[msb_to_le(kk, K)] = counts[a:b]  # indexed by LE bin
+            exp = dense[:, s]
+        else:
+            col[kk] = counts[a:b]  # indexed by MSB key
+            d = dense[:, s].contiguous()[le_all]  # dense count of every MSB key
+            exp = torch.where(canon, d + d[rc_all], torch.zeros_like(d))
+            del d
         # a key listed twice would leave one of its two counts in col: the sums differ
         assert int(counts[a:b].to(torch.int64).sum()) == int(col.to(torch.int64).sum()), \
             "record %d: a key listed twice" % s
-        assert torch.equal(col, dense[:, s]), "record %d: forward canonical lists != dense histogram" % s
+        assert torch.equal(col, exp), "record %d: canonical lists (forward=%s) != dense histogram" % (s, forward)
         total += b - a
-        del kk, le
+        del kk, exp
     assert total == off_h[-1]
     del keys, counts, off, dense, inv
+    if not forward:
+        del le_all, rc_all, canon
     torch.cuda.empty_cache()
     return total
 
@@ -92,19 +122,30 @@ def synth():
     return genome_synth
 
 
-@pytest.mark.parametrize("soft", [False, True])
-def test_c4_forward_k13_equals_dense(kmc, cuda, synth, soft):
+@pytest.fixture(scope="module")
+def c4(cuda, synth):
     import torch
     data, idx, lens = synth.grch38_like(torch, cuda, GBASES)
-    distinct = check_forward_equals_dense(kmc, data, idx, soft)
-    assert distinct > 25 * 10_000_000  # each record's ~124 Mbase fill most of its 67 M bins
+    yield data, idx
     del data, idx
     torch.cuda.empty_cache()
 
 
-def test_c4r_forward_k13_equals_dense(kmc, cuda, synth):
+@pytest.fixture(scope="module")
+def c4r(cuda, synth):
     import torch
     data, idx, lens, _ = synth.repeat_genome(torch, cuda, GBASES)
-    check_forward_equals_dense(kmc, data, idx, True)
+    yield data, idx
     del data, idx
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("soft,forward", [(False, True), (True, True), (True, False)])
+def test_c4_k13_equals_dense(kmc, c4, soft, forward):
+    distinct = check_against_dense(kmc, *c4, soft, forward)
+    assert distinct > 25 * 10_000_000  # each record's ~124 Mbase fill most of its 67 M bins
+
+
+@pytest.mark.parametrize("forward", [True, False])
+def test_c4r_k13_equals_dense(kmc, c4r, forward):
+    check_against_dense(kmc, *c4r, True, forward)
