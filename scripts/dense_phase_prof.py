@@ -133,7 +133,15 @@ def run(worlds, steps):
                "piece0_sync_us(median after last wave)": float(np.median(p0s - p0w.max(1))),
                "piece0_flush_us(median)": float(np.median(p0f - p0s)),
                "exit_us": [float(exit_.min()), float(np.median(exit_)), float(exit_.max())],
-               "exit_p90_us": float(pct(list(exit_), 0.9))}
+               "exit_p90_us": float(pct(list(exit_), 0.9)),
+               # (round 6) per XCD (workgroup id mod 8, the dispatcher's round robin):
+               # median / max exit and median duration (exit - entry)
+               "per_xcd_exit_med_max_dur_us": [
+                   [round(float(np.median(exit_[np.nonzero(used)[0] % 8 == x])), 1),
+                    round(float(exit_[np.nonzero(used)[0] % 8 == x].max()), 1),
+                    round(float(np.median((exit_ - entry)[np.nonzero(used)[0] % 8 == x])), 1)] for x in range(8)],
+               "duration_us_min_med_max": [float((exit_ - entry).min()), float(np.median(exit_ - entry)),
+                                           float((exit_ - entry).max())]}
         # the hot-half scans (barriers every kHm3Scan tiles per wave): per segment the
         # spread of the waves' arrivals, and the scan itself (single-piece workgroups)
         one = b[~two]
