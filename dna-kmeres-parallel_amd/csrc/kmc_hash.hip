@@ -403,6 +403,15 @@ __global__ __launch_bounds__(kWalkBlock) void canon_count_kernel(HParams p) {
 //   cnt[2][kMaxBk + 1]  bucket counts -> offsets (double-buffered by round parity)
 //   cur[kMaxBk]         global position of each bucket's next entry
 //   del[kMaxBk]         this round: global position of stage index 0 of each run
+// Entries go out as h (lists = false: coarse buckets) or as list values (lists).
+// Round 6: pin() (an empty asm that redefines the prefetched next chunk's
+// registers) runs before the write-out, so the compiler waits for those loads
+// there -- issued a round earlier -- instead of at the loop latch behind this
+// round's stores: vmcnt counts stores on gfx9 and the write-out issues a variable
+// number of them, so a wait placed after them is vmcnt(0), i.e. for their
+// acknowledgements, once per 16 K windows.  The write-out is one call (lists a
+// uniform flag, not two calls): with two, the structurized CFG has a path through
+// neither call -- so through no pin -- and the compiler kept a wait on it.
 struct Stage {
     unsigned long long *stage;  // [kRound]
     uint32_t (*cnt)[kMaxBk + 1];
@@ -410,9 +419,9 @@ struct Stage {
     unsigned long long *del;
 };
 
-template <class Bk, class Out>
+template <class Bk, class Pin>
 __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, const unsigned long long (&h)[16],
-                                             uint32_t vm, Bk bk, Out out, uint64_t *dst) {
+                                             uint32_t vm, Bk bk, bool lists, uint64_t *dst, Pin pin) {
     const int tid = threadIdx.x, lane = tid & 63;
     uint32_t *cn = s.cnt[par];
     uint32_t rk[8];
@@ -457,9 +466,17 @@ __device__ __forceinline__ void staged_round(const Stage &s, int par, int nbk, c
     uint32_t *nx = s.cnt[par ^ 1];  // next round's counts (last read before this round's first barrier)
     for (int b = tid; b <= nbk; b += kWalkBlock) nx[b] = 0u;
     lds_barrier();
-    for (uint32_t i = tid; i < total; i += kWalkBlock) {
-        const unsigned long long x = s.stage[i];
-        dst[s.del[bk(x)] + i] = out(x);
+    pin();
+    if (lists) {  // (uniform) buckets are the lists: list values
+        for (uint32_t i = tid; i < total; i += kWalkBlock) {
+            const unsigned long long x = s.stage[i];
+            dst[s.del[bk(x)] + i] = list_value(x);
+        }
+    } else {
+        for (uint32_t i = tid; i < total; i += kWalkBlock) {
+            const unsigned long long x = s.stage[i];
+            dst[s.del[bk(x)] + i] = x;
+        }
     }
     // the next round writes stage / del only after two barriers, which every
     // thread reaches after this write-out
@@ -643,17 +660,21 @@ __global__ __launch_bounds__(kWalkBlock) void canon_coarse_kernel(HParams p) {
         uint64_t *dst = lg > lgc ? p.ent_c : p.ent;
         const auto bk = [lgc](unsigned long long x) { return top_bits(x, lgc); };
         const int64_t c0 = ps >> 4, c1 = ((pe - 1) >> 4) + 1;
+        const bool lists = __builtin_amdgcn_readfirstlane(lg) <= lgc;
         ChunkRaw nx = chunk_raw(p, (c0 + threadIdx.x) << 4);
+        const auto pin = [&nx]() {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                asm volatile("" : "+v"(nx.r[i].x), "+v"(nx.r[i].y), "+v"(nx.r[i].z), "+v"(nx.r[i].w));
+        };
+        pin();
         for (int64_t cb = c0; cb < c1; cb += kWalkBlock) {
             const int64_t c = cb + threadIdx.x;
             unsigned long long h[16];
             const ChunkRaw cr = nx;
             nx = chunk_raw(p, (c + kWalkBlock) << 4);  // next round's chunk
             const uint32_t vm = chunk_keys<FWD, BIGK>(p, cr, c << 4, ps, pe, rend, h);  // (past the piece: vm = 0, h defined)
-            if (lg > lgc)
-                staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return x; }, dst);
-            else  // buckets are the lists
-                staged_round(st, par, nbk, h, vm, bk, [](unsigned long long x) { return list_value(x); }, dst);
+            staged_round(st, par, nbk, h, vm, bk, lists, dst, pin);
             par ^= 1;
         }
         __syncthreads();
@@ -693,24 +714,41 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
     Ring8 rg;
     rg.init(&R, p.ent, lf, p.list_start[lb + (threadIdx.x >> (10 - lf))]);
     __syncthreads();
-    // the next round's entries are loaded before this round is ranked and flushed
-    // (one workgroup per CU whose waves meet at every round's barriers
-    // would otherwise wait on HBM once per round)
-    unsigned long long xn[8];
-    const auto fetch = [&](uint64_t i0) {
+    // The entries of the next two rounds are in flight while this round is ranked
+    // and flushed (one workgroup per CU whose waves meet at every round's barriers
+    // would otherwise wait on HBM once per round).  Round 6: two register sets that
+    // swap roles every round (no copy of registers still loading), the next round's
+    // set pinned (as staged_round's pin) before this round's flush, so no wait
+    // follows the flush's stores, and unconditional raw buffer loads -- the range
+    // check returns zeros from a1 on -- so every round issues its 8 loads and the
+    // compiler's waits on them count exactly (per-lane guarded loads made it
+    // vmcnt(0)).  K3b 9.10-9.19 -> 9.00-9.03 ms on C4, with K3a's pin 6.50-6.60 ->
+    // 6.42-6.47 ms (profiles/r06s_store_ack_pins_ab.txt).
+    const auto fetch = [&](unsigned long long (&xn)[8], uint64_t i0) {
+        const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)i0) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(i0 >> 32)) << 32);
+        int64_t nrec = ((int64_t)a1 - (int64_t)u) * 8;
+        nrec = nrec < 0 ? 0 : (nrec > (1ll << 31) ? (1ll << 31) : nrec);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.ent_c + u, (short)0, (int)nrec, 0x00020000);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
-            xn[j] = i < a1 ? p.ent_c[i] : 0ull;
+            const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, (j * kWalkBlock + (int)threadIdx.x) * 8, 0, 0);
+            xn[j] = (unsigned long long)x[0] | ((unsigned long long)x[1] << 32);
         }
     };
-    fetch(a0);
-    for (uint64_t i0 = a0; i0 < a1; i0 += 8 * kWalkBlock) {
+    const auto pin = [](unsigned long long (&xn)[8]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(xn[j]));
+    };
+    // round i0: its entries cur (loaded); cur is refilled with round i0 + 2 rounds' and
+    // nxt (round i0 + 1 round's) is waited for before this round's stores
+    const auto round = [&](uint64_t i0, unsigned long long (&cur)[8], unsigned long long (&nxt)[8]) {
         unsigned long long v[8], x[8];
         uint32_t bk[8], vm = 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = xn[j];
-        if (i0 + 8 * kWalkBlock < a1) fetch(i0 + 8 * kWalkBlock);
+        for (int j = 0; j < 8; ++j) x[j] = cur[j];
+        fetch(cur, i0 + 16 * kWalkBlock);  // (past a1: zeros, never counted)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint64_t i = i0 + (uint64_t)j * kWalkBlock + threadIdx.x;
@@ -719,7 +757,17 @@ __global__ __launch_bounds__(kWalkBlock) void canon_fine_kernel(HParams p) {
             v[j] = list_value(x[j]);
         }
         rg.add<8>(v, bk, vm);
+        pin(nxt);
         rg.round_end();
+    };
+    unsigned long long xa[8], xb[8];
+    fetch(xa, a0);
+    pin(xa);
+    fetch(xb, a0 + 8 * kWalkBlock);
+    for (uint64_t i0 = a0; i0 < a1; i0 += 16 * kWalkBlock) {
+        round(i0, xa, xb);
+        if (i0 + 8 * kWalkBlock >= a1) break;
+        round(i0 + 8 * kWalkBlock, xb, xa);
     }
     rg.finish();
 }
