@@ -52,6 +52,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=14)  # the clocks settle over ~10 launches (after the guard step)
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed: histogram launches back to back for this long (wall) after the correctness "
+                         "guard and before the W warm-up steps, so that the GPU clock has ramped up from the "
+                         "guard's host-side idle (0 = none); the timed region is unchanged")
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: --records records in total, byte-range shards; weak: --records per GPU")
@@ -366,6 +370,22 @@ def main():
         got, _ = kmc.count_dense(sl, torch.tensor([0, s_len + 1], dtype=torch.int64, device=dev), k)
         if not np.array_equal(got.view(-1).cpu().numpy().astype(np.int64), exp):
             raise SystemExit("count check failed: a 1 Mbase slice differs from its host histogram")
+    # clock settle (round 6): the guard's host work above idles the GPU, and the clock
+    # then ramps over ~10-25 launches of this kernel -- with the driver's --warmup 5
+    # the first ~10 timed steps were still ramping (profiles/r06w_bench5.json:
+    # 2.36 -> 2.11 ms over the 20 steps).  Untimed histogram launches (this rank's
+    # count alone, no collective, so ranks may differ in how many they run) for
+    # settle_ms of wall time first; then the W warm-up steps and the K timed steps
+    # exactly as before.
+    settle_n = 0
+    if args.settle_ms > 0:
+        t_s = time.perf_counter()
+        while (time.perf_counter() - t_s) * 1e3 < args.settle_ms and settle_n < 4096:
+            for _ in range(4):
+                count(last)
+            settle_n += 4
+            torch.cuda.synchronize()
+    args.settle_launches = settle_n
     for i in range(args.warmup):
         step(i + 1)
     drain()
@@ -544,6 +564,11 @@ def finalize(args, world, rank, backend, data, matrix, L, k, n_tot, win, elapsed
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle": {"ms": getattr(args, "settle_ms", 0.0), "launches": getattr(args, "settle_launches", 0),
+                   "how": "untimed histogram launches back to back (this rank's count only) after the correctness "
+                          "guard and before the W warm-up steps, for settle.ms of wall time, so that the GPU "
+                          "clock has ramped up from the guard's host-side idle; the timed region is exactly K "
+                          "full steps either way"},
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": args.scaling,

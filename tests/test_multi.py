@@ -299,6 +299,8 @@ def test_gloo_world2_bench_line_fields():
     r = res[0]
     assert r["n_gpus"] == 2 and r["config"]["rccl_world"] == 2 and r["config"]["backend"] == "gloo"
     assert "reserved_cus" in r["config"] and "rccl_max_channels" in r["config"]
+    # the untimed clock settle is reported beside W (finalize alone ran none)
+    assert r["warmup"] == 14 and r["settle"]["ms"] == 150.0 and r["settle"]["launches"] == 0
     # max over ranks: rank 1's elapsed and kernel time
     assert abs(r["ms_per_step"] - 0.02 / 5 * 1e3) < 1e-9 and r["roofline"]["kernel_ms"] == 1.5
     rf = r["roofline"]
